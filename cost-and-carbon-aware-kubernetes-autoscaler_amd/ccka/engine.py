@@ -1,0 +1,99 @@
+"""Python handle on libccka.so (the HIP rollout engine) through its C ABI.
+
+There is no CPU fallback: constructing an Engine without the built library or
+without a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .world import TRAJ_DTYPE, ScenarioSet, WorldSpec, alloc_results
+
+
+class Engine:
+    def __init__(self, device: int = 0, lib_path: str | None = None):
+        self.lib = abi.load_engine(lib_path)
+        abi.check_sizes(self.lib)
+        self.ctx = C.c_void_p()
+        abi.check(self.lib.ccka_open(C.byref(self.ctx), device), "ccka_open")
+        self.n = 0
+        self.T = 0
+        self.D = 0
+
+    def _chk(self, rc, what):
+        abi.check(rc, what, self.lib, self.ctx)
+
+    def close(self):
+        if self.ctx:
+            self.lib.ccka_close(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_world(self, spec: WorldSpec):
+        w = spec.to_c()
+        self._chk(self.lib.ccka_set_world(self.ctx, C.byref(w)), "ccka_set_world")
+        self.T = spec.n_steps
+        self.D = len(spec.deploys)
+
+    def set_scenarios(self, sc: ScenarioSet):
+        s = sc.to_c()
+        self._chk(self.lib.ccka_set_scenarios(self.ctx, C.byref(s)), "ccka_set_scenarios")
+        self.n = sc.n
+
+    def set_load(self, load: np.ndarray):
+        a = np.ascontiguousarray(load, np.int32)
+        self._chk(self.lib.ccka_set_load(self.ctx, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size),
+                  "ccka_set_load")
+
+    def gen_load(self, gen: abi.TraceGen):
+        self._chk(self.lib.ccka_gen_load(self.ctx, C.byref(gen)), "ccka_gen_load")
+
+    def get_load(self) -> np.ndarray:
+        a = np.zeros((self.T, self.D, self.n), np.int32)
+        self._chk(self.lib.ccka_get_load(self.ctx, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size),
+                  "ccka_get_load")
+        return a
+
+    def rollout(self, trajectory: bool = False):
+        self._chk(self.lib.ccka_rollout(self.ctx, int(trajectory)), "ccka_rollout")
+
+    def rollout_async(self, trajectory: bool = False):
+        self._chk(self.lib.ccka_rollout_async(self.ctx, int(trajectory)), "ccka_rollout_async")
+
+    def sync(self):
+        self._chk(self.lib.ccka_sync(self.ctx), "ccka_sync")
+
+    def kernel_ms(self) -> float:
+        v = C.c_double()
+        self._chk(self.lib.ccka_last_kernel_ms(self.ctx, C.byref(v)), "ccka_last_kernel_ms")
+        return v.value
+
+    def results(self) -> dict:
+        arrays, r = alloc_results(self.n)
+        self._chk(self.lib.ccka_get_results(self.ctx, C.byref(r)), "ccka_get_results")
+        return arrays
+
+    def trajectory(self) -> np.ndarray:
+        a = np.zeros((self.T, self.n), TRAJ_DTYPE)
+        self._chk(self.lib.ccka_get_trajectory(self.ctx, a.ctypes.data_as(C.POINTER(abi.TrajRec)),
+                                               a.size), "ccka_get_trajectory")
+        return a
+
+    def totals(self) -> abi.Totals:
+        t = abi.Totals()
+        self._chk(self.lib.ccka_get_totals(self.ctx, C.byref(t)), "ccka_get_totals")
+        return t
+
+    def device_info(self):
+        name = C.create_string_buffer(256)
+        cus = C.c_int32()
+        self._chk(self.lib.ccka_device_info(self.ctx, name, 256, C.byref(cus)), "ccka_device_info")
+        return name.value.decode(), cus.value

@@ -1,0 +1,583 @@
+// ccka_abi.cpp — the C ABI of libccka.so (include/ccka.h).
+//
+// Owns the device buffers of one context, validates the world against the
+// engine's limits, chooses the launch geometry (LDS budget per workgroup from
+// the catalog, the price-tile span and the NodeClaim scratch) and drives the
+// kernels in rollout.hip on the context's stream. Multi-GPU: one context per
+// GPU; totals are summed with RCCL over xGMI (the only cross-GPU exchange:
+// scenarios are independent).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/ccka.h"
+#include "kparams.h"
+
+using namespace ccka;
+
+struct ccka_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+  int cus = 0;
+  char name[128] = {0};
+  // world
+  bool have_world = false;
+  ccka_world hw{};
+  ccka_world* d_world = nullptr;
+  ccka_itype* d_types = nullptr;
+  int32_t* d_price = nullptr;
+  double* d_ci_gpwh = nullptr;
+  double* d_ci_gpwmin = nullptr;
+  int prov[CCKA_MAX_DEPLOY] = {0};
+  // scenarios
+  bool have_sc = false;
+  int64_t N = 0, first_id = 0;
+  std::vector<uint8_t> h_region;
+  uint8_t* d_region = nullptr;
+  int16_t* d_target = nullptr;
+  int16_t* d_maxr = nullptr;
+  int16_t* d_dstab = nullptr;
+  int16_t* d_resetca = nullptr;
+  uint8_t* d_pswitch = nullptr;
+  double* d_cw = nullptr;
+  uint8_t* d_capsel = nullptr;
+  // traces / outputs
+  int32_t* d_load = nullptr;
+  int64_t load_count = 0;
+  bool have_load = false;
+  void* d_res = nullptr;  // one allocation, SoA carve
+  KParams kp{};
+  ccka_traj_rec* d_traj = nullptr;
+  int64_t traj_count = 0;
+  bool traj_valid = false;
+  void* d_parts = nullptr;
+  ccka_totals* d_totals = nullptr;
+  int32_t* d_sinq = nullptr;
+  ncclComm_t comm = nullptr;
+  double last_ms = 0.0;
+  bool ran = false;
+};
+
+static int fail(ccka_ctx* c, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+static int fail(ccka_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(c, x)                                                              \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess)                                                         \
+      return fail((c), CCKA_EHIP, "%s: %s", #x, hipGetErrorString(e_));          \
+  } while (0)
+
+template <class T>
+static void dfree(T*& p) {
+  if (p) { (void)hipFree((void*)p); p = nullptr; }
+}
+
+template <class T>
+static int dupload(ccka_ctx* c, T*& dst, const T* src, size_t count) {
+  dfree(dst);
+  if (!src || count == 0) return CCKA_OK;
+  if (hipMalloc((void**)&dst, sizeof(T) * count) != hipSuccess)
+    return fail(c, CCKA_ENOMEM, "hipMalloc %zu bytes failed", sizeof(T) * count);
+  HIPCHK(c, hipMemcpyAsync(dst, src, sizeof(T) * count, hipMemcpyHostToDevice, c->stream));
+  return CCKA_OK;
+}
+
+extern "C" {
+
+int32_t ccka_abi_version(void) { return CCKA_ABI_VERSION; }
+
+int32_t ccka_struct_sizes(int64_t* out, int32_t n) {
+  const int64_t s[] = {sizeof(ccka_itype),    sizeof(ccka_pool),    sizeof(ccka_deployment),
+                       sizeof(ccka_world),    sizeof(ccka_scenarios), sizeof(ccka_results),
+                       sizeof(ccka_traj_rec), sizeof(ccka_totals),  sizeof(ccka_trace_gen)};
+  const int32_t m = (int32_t)(sizeof s / sizeof s[0]);
+  int32_t k = 0;
+  for (; k < m && k < n; ++k) out[k] = s[k];
+  return k;
+}
+
+const char* ccka_last_error(const ccka_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ccka_open(ccka_ctx** out, int device_ordinal) {
+  if (!out) return CCKA_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return CCKA_ENODEV;
+  if (device_ordinal < 0 || device_ordinal >= ndev) return CCKA_ENODEV;
+  if (hipSetDevice(device_ordinal) != hipSuccess) return CCKA_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) return CCKA_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CCKA_ENODEV;
+  ccka_ctx* c = new (std::nothrow) ccka_ctx();
+  if (!c) return CCKA_ENOMEM;
+  c->device = device_ordinal;
+  c->cus = prop.multiProcessorCount;
+  std::snprintf(c->name, sizeof c->name, "%s (%s)", prop.name, prop.gcnArchName);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    delete c;
+    return CCKA_EHIP;
+  }
+  // sine table of the synthetic load generator (SEMANTICS.md §4)
+  int32_t sinq[1440];
+  for (int m = 0; m < 1440; ++m) sinq[m] = (int32_t)std::lround(65536.0 * std::sin(2.0 * M_PI * (double)m / 1440.0));
+  if (dupload(c, c->d_sinq, sinq, 1440) != CCKA_OK || hipStreamSynchronize(c->stream) != hipSuccess) {
+    ccka_close(c);
+    return CCKA_EHIP;
+  }
+  *out = c;
+  return CCKA_OK;
+}
+
+static void free_results(ccka_ctx* c) {
+  dfree(c->d_res);
+  dfree(c->d_traj);
+  dfree(c->d_parts);
+  c->traj_count = 0;
+  c->traj_valid = false;
+}
+
+void ccka_close(ccka_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  dfree(c->d_world); dfree(c->d_types); dfree(c->d_price); dfree(c->d_ci_gpwh); dfree(c->d_ci_gpwmin);
+  dfree(c->d_region); dfree(c->d_target); dfree(c->d_maxr); dfree(c->d_dstab); dfree(c->d_resetca);
+  dfree(c->d_pswitch); dfree(c->d_cw); dfree(c->d_capsel); dfree(c->d_load); dfree(c->d_totals);
+  dfree(c->d_sinq);
+  free_results(c);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static bool rules_ok(const ccka_hpa_rules& r) {
+  if (r.select < 0 || r.select > 2 || r.n_policies < 0 || r.n_policies > 2) return false;
+  if (r.stab_window_s < 0 || r.stab_window_s > CCKA_HIST * CCKA_STEP_SECONDS) return false;
+  for (int i = 0; i < r.n_policies; ++i) {
+    const ccka_hpa_policy& p = r.policies[i];
+    if ((p.type != CCKA_HPA_PODS && p.type != CCKA_HPA_PERCENT) || p.value < 0 || p.period_s < 0 ||
+        p.period_s > CCKA_HIST * CCKA_STEP_SECONDS)
+      return false;
+  }
+  return true;
+}
+
+int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
+  if (!c || !w) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (w->n_steps < 1 || w->n_steps > 65535) return fail(c, CCKA_EINVAL, "n_steps out of range");
+  if (w->max_nodes < 1 || w->max_nodes > CCKA_MAX_NODES) return fail(c, CCKA_EINVAL, "max_nodes out of range");
+  if (w->n_types < 1 || w->n_types > CCKA_MAX_TYPES || !w->types) return fail(c, CCKA_EINVAL, "catalog invalid");
+  if (w->n_zones < 1 || w->n_zones > CCKA_MAX_ZONES) return fail(c, CCKA_EINVAL, "n_zones out of range");
+  if (w->n_regions < 1 || w->n_regions > CCKA_MAX_REGIONS) return fail(c, CCKA_EINVAL, "n_regions out of range");
+  if (w->n_pools < 1 || w->n_pools > CCKA_MAX_POOLS) return fail(c, CCKA_EINVAL, "n_pools out of range");
+  if (w->n_deploy < 1 || w->n_deploy > CCKA_MAX_DEPLOY) return fail(c, CCKA_EINVAL, "n_deploy out of range");
+  if (!w->price_uph || !w->ci_gpwh || !w->ci_gpwmin) return fail(c, CCKA_EINVAL, "tiles missing");
+  if (w->base_type < 0 || w->base_type >= w->n_types) return fail(c, CCKA_EINVAL, "base_type out of range");
+  if (w->provision_delay_steps < 0 || w->start_minute < 0) return fail(c, CCKA_EINVAL, "negative timing");
+  for (int k = 0; k < w->n_types; ++k) {
+    const ccka_itype& t = w->types[k];
+    if (t.vcpu < 0 || t.alloc_cpu_m <= 0 || t.alloc_mem_mi < 0 || t.max_pods < 0)
+      return fail(c, CCKA_EINVAL, "catalog entry %d invalid", k);
+  }
+  for (int d = 0; d < w->n_deploy; ++d) {
+    const ccka_deployment& dp = w->deploy[d];
+    if (dp.scaler < 0 || dp.scaler > 2 || dp.cap_sel == 0 || dp.cap_sel > 3 || dp.req_cpu_m < 0 ||
+        dp.req_mem_mi < 0 || dp.replicas0 < 0)
+      return fail(c, CCKA_EINVAL, "deployment %d invalid", d);
+    if (dp.scaler == CCKA_SCALER_HPA && (dp.req_cpu_m <= 0 || dp.target_util_pct <= 0))
+      return fail(c, CCKA_EINVAL, "HPA deployment %d needs cpu request and target", d);
+    if (dp.scaler == CCKA_SCALER_KEDA && dp.keda_threshold <= 0)
+      return fail(c, CCKA_EINVAL, "KEDA deployment %d needs threshold", d);
+    if (!rules_ok(dp.up) || !rules_ok(dp.down))
+      return fail(c, CCKA_EINVAL, "deployment %d behavior outside the %d s history", d,
+                  CCKA_HIST * CCKA_STEP_SECONDS);
+  }
+  c->hw = *w;
+  const int K = w->n_types, Z = w->n_zones, R = w->n_regions;
+  int rc;
+  if ((rc = dupload(c, c->d_types, w->types, (size_t)K)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_price, w->price_uph, (size_t)R * 24 * K * Z * 2)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_ci_gpwh, w->ci_gpwh, (size_t)R * 24)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_ci_gpwmin, w->ci_gpwmin, (size_t)R * 24)) != CCKA_OK) return rc;
+  ccka_world dw = *w;
+  dw.types = nullptr; dw.ci_gpwh = nullptr; dw.ci_gpwmin = nullptr; dw.price_uph = nullptr;
+  if ((rc = dupload(c, c->d_world, &dw, 1)) != CCKA_OK) return rc;
+  // provisioning order: req_cpu desc, req_mem desc, index asc
+  const int D = w->n_deploy;
+  for (int d = 0; d < D; ++d) c->prov[d] = d;
+  std::stable_sort(c->prov, c->prov + D, [&](int a, int b) {
+    const ccka_deployment &A = w->deploy[a], &B = w->deploy[b];
+    if (A.req_cpu_m != B.req_cpu_m) return A.req_cpu_m > B.req_cpu_m;
+    return A.req_mem_mi > B.req_mem_mi;
+  });
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->have_world = true;
+  c->have_load = false;
+  c->traj_valid = false;
+  c->ran = false;
+  return CCKA_OK;
+}
+
+static int alloc_results(ccka_ctx* c) {
+  free_results(c);
+  const int64_t N = c->N;
+  // 8-byte fields first, then 4-byte fields; each array 256-B aligned
+  auto up = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  const int64_t b8 = up(N * 8), b4 = up(N * 4);
+  const int64_t total = 4 * b8 + 10 * b4;
+  if (hipMalloc(&c->d_res, (size_t)total) != hipSuccess) return fail(c, CCKA_ENOMEM, "results alloc");
+  char* p = (char*)c->d_res;
+  KParams& k = c->kp;
+  k.cost = (int64_t*)p; p += b8;
+  k.energy = (double*)p; p += b8;
+  k.gco2 = (double*)p; p += b8;
+  k.pend_min = (int64_t*)p; p += b8;
+  k.slo = (int32_t*)p; p += b4;
+  k.nmin_spot = (int32_t*)p; p += b4;
+  k.nmin_od = (int32_t*)p; p += b4;
+  k.launches = (int32_t*)p; p += b4;
+  k.deletions = (int32_t*)p; p += b4;
+  k.peak_nodes = (int32_t*)p; p += b4;
+  k.final_reps = (int32_t*)p; p += b4;
+  k.final_nodes = (int32_t*)p; p += b4;
+  k.last_choice = (uint32_t*)p; p += b4;
+  k.hash = (uint32_t*)p; p += b4;
+  if (hipMalloc(&c->d_parts, 1024 * sizeof(long long) * 10) != hipSuccess) return fail(c, CCKA_ENOMEM, "parts alloc");
+  if (!c->d_totals && hipMalloc((void**)&c->d_totals, sizeof(ccka_totals)) != hipSuccess)
+    return fail(c, CCKA_ENOMEM, "totals alloc");
+  return CCKA_OK;
+}
+
+int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
+  if (!c || !sc) return CCKA_EINVAL;
+  if (!c->have_world) return fail(c, CCKA_ESTATE, "set_world first");
+  if (sc->n < 1 || sc->n > (int64_t)1 << 31) return fail(c, CCKA_EINVAL, "scenario count out of range");
+  (void)hipSetDevice(c->device);
+  const size_t n = (size_t)sc->n;
+  if (sc->region) {
+    for (size_t i = 0; i < n; ++i)
+      if (sc->region[i] >= c->hw.n_regions) return fail(c, CCKA_EINVAL, "region %u out of range", sc->region[i]);
+    c->h_region.assign(sc->region, sc->region + n);
+  } else {
+    c->h_region.clear();
+  }
+  if (sc->cap_sel)
+    for (size_t i = 0; i < n; ++i)
+      if (sc->cap_sel[i] == 0 || sc->cap_sel[i] > 3) return fail(c, CCKA_EINVAL, "cap_sel invalid");
+  if (sc->target_util_pct)
+    for (size_t i = 0; i < n; ++i)
+      if (sc->target_util_pct[i] <= 0) return fail(c, CCKA_EINVAL, "target_util_pct must be > 0");
+  if (sc->down_stab_s)
+    for (size_t i = 0; i < n; ++i)
+      if (sc->down_stab_s[i] < 0 || sc->down_stab_s[i] > CCKA_HIST * CCKA_STEP_SECONDS)
+        return fail(c, CCKA_EINVAL, "down_stab_s outside the history window");
+  int rc;
+  if ((rc = dupload(c, c->d_region, sc->region, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_target, sc->target_util_pct, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_maxr, sc->max_replicas, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_dstab, sc->down_stab_s, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_resetca, sc->reset_ca_s, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_pswitch, sc->peak_switch, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_cw, sc->carbon_weight, n)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_capsel, sc->cap_sel, n)) != CCKA_OK) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->N = sc->n;
+  c->first_id = sc->first_id;
+  if ((rc = alloc_results(c)) != CCKA_OK) return rc;
+  dfree(c->d_load);
+  c->have_load = false;
+  c->have_sc = true;
+  c->ran = false;
+  return CCKA_OK;
+}
+
+static int ensure_load(ccka_ctx* c) {
+  const int64_t cnt = (int64_t)c->hw.n_steps * c->hw.n_deploy * c->N;
+  if (c->d_load && c->load_count == cnt) return CCKA_OK;
+  dfree(c->d_load);
+  if (hipMalloc((void**)&c->d_load, (size_t)cnt * 4) != hipSuccess)
+    return fail(c, CCKA_ENOMEM, "load alloc %lld ints", (long long)cnt);
+  c->load_count = cnt;
+  return CCKA_OK;
+}
+
+int ccka_set_load(ccka_ctx* c, const int32_t* load, int64_t count) {
+  if (!c || !load) return CCKA_EINVAL;
+  if (!c->have_sc) return fail(c, CCKA_ESTATE, "set_scenarios first");
+  (void)hipSetDevice(c->device);
+  int rc;
+  if ((rc = ensure_load(c)) != CCKA_OK) return rc;
+  if (count != c->load_count) return fail(c, CCKA_EINVAL, "load count %lld != T*D*N %lld", (long long)count, (long long)c->load_count);
+  HIPCHK(c, hipMemcpyAsync(c->d_load, load, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->have_load = true;
+  return CCKA_OK;
+}
+
+int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
+  if (!c || !g) return CCKA_EINVAL;
+  if (!c->have_sc) return fail(c, CCKA_ESTATE, "set_scenarios first");
+  if (g->base_hi < g->base_lo || g->amp_hi_pm < g->amp_lo_pm || g->burst_len < 0)
+    return fail(c, CCKA_EINVAL, "trace generator ranges invalid");
+  (void)hipSetDevice(c->device);
+  int rc;
+  if ((rc = ensure_load(c)) != CCKA_OK) return rc;
+  GenParams gp{};
+  gp.out = c->d_load;
+  gp.sinq = c->d_sinq;
+  gp.n = c->N;
+  gp.first_id = c->first_id;
+  gp.seed = g->seed;
+  gp.T = c->hw.n_steps;
+  gp.D = c->hw.n_deploy;
+  gp.base_lo = g->base_lo; gp.base_hi = g->base_hi;
+  gp.amp_lo = g->amp_lo_pm; gp.amp_hi = g->amp_hi_pm;
+  gp.noise = g->noise_pm; gp.burst_prob = g->burst_prob_pm;
+  gp.burst_mult = g->burst_mult_pm; gp.burst_len = g->burst_len;
+  HIPCHK(c, launch_gen_load(gp, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->have_load = true;
+  return CCKA_OK;
+}
+
+int ccka_get_load(ccka_ctx* c, int32_t* load, int64_t count) {
+  if (!c || !load) return CCKA_EINVAL;
+  if (!c->have_load) return fail(c, CCKA_ESTATE, "no load on device");
+  if (count != c->load_count) return fail(c, CCKA_EINVAL, "load count mismatch");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(load, c->d_load, (size_t)count * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+static int plan_launch(ccka_ctx* c, int* block, size_t* lds) {
+  const ccka_world& w = c->hw;
+  const int B = 256;
+  int span = 1;
+  if (!c->h_region.empty()) {
+    for (int64_t b = 0; b < c->N; b += B) {
+      const int64_t e = std::min<int64_t>(c->N, b + B);
+      int lo = 255, hi = 0;
+      for (int64_t i = b; i < e; ++i) { lo = std::min<int>(lo, c->h_region[i]); hi = std::max<int>(hi, c->h_region[i]); }
+      span = std::max(span, hi - lo + 1);
+    }
+  }
+  int dmax, nmax;
+  kernel_dims(w.n_deploy, w.max_nodes, &dmax, &nmax);
+  auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t K = (size_t)w.n_types;
+  size_t off = up16(K * sizeof(ccka_itype));
+  KParams& k = c->kp;
+  k.lds_off_cap1 = (int32_t)off;
+  off = up16(off + K * 4);
+  k.lds_off_tile = (int32_t)off;
+  off = up16(off + (size_t)span * K * w.n_zones * 2 * 4);
+  k.lds_off_claims = (int32_t)off;
+  off = up16(off + (size_t)(B / 64) * nmax * (7 + dmax) * 4);
+  k.lds_off_misc = (int32_t)off;
+  off += 16;
+  if (off > 160 * 1024) return fail(c, CCKA_EINVAL, "LDS budget %zu B exceeds 160 KiB (catalog %zu types, span %d)", off, K, span);
+  k.span = span;
+  *block = B;
+  *lds = off;
+  return CCKA_OK;
+}
+
+int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
+  if (!c) return CCKA_EINVAL;
+  if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
+  if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
+  (void)hipSetDevice(c->device);
+  const ccka_world& w = c->hw;
+  int block = 256;
+  size_t lds = 0;
+  int rc;
+  if ((rc = plan_launch(c, &block, &lds)) != CCKA_OK) return rc;
+  KParams& k = c->kp;
+  k.w = c->d_world;
+  k.types = c->d_types;
+  k.price = c->d_price;
+  k.ci_gpwh = c->d_ci_gpwh;
+  k.ci_gpwmin = c->d_ci_gpwmin;
+  k.load = c->d_load;
+  k.region = c->d_region;
+  k.target = c->d_target;
+  k.maxr = c->d_maxr;
+  k.down_stab = c->d_dstab;
+  k.reset_ca = c->d_resetca;
+  k.pswitch = c->d_pswitch;
+  k.cw = c->d_cw;
+  k.cap_sel = c->d_capsel;
+  k.traj = nullptr;
+  if (trajectory) {
+    const int64_t cnt = (int64_t)w.n_steps * c->N;
+    if (c->traj_count != cnt) {
+      dfree(c->d_traj);
+      if (hipMalloc((void**)&c->d_traj, (size_t)cnt * sizeof(ccka_traj_rec)) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "trajectory alloc");
+      c->traj_count = cnt;
+    }
+    k.traj = c->d_traj;
+  }
+  k.N = c->N;
+  k.T = w.n_steps;
+  k.D = w.n_deploy;
+  k.K = w.n_types;
+  k.Z = w.n_zones;
+  k.R = w.n_regions;
+  k.P = w.n_pools;
+  k.maxn = w.max_nodes;
+  for (int d = 0; d < CCKA_MAX_DEPLOY; ++d) k.prov[d] = c->prov[d];
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->traj_valid = trajectory != 0;
+  c->ran = true;
+  return CCKA_OK;
+}
+
+int ccka_sync(ccka_ctx* c) {
+  if (!c) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->ran) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->last_ms = ms;
+  }
+  return CCKA_OK;
+}
+
+int ccka_rollout(ccka_ctx* c, int32_t trajectory) {
+  int rc = ccka_rollout_async(c, trajectory);
+  if (rc != CCKA_OK) return rc;
+  return ccka_sync(c);
+}
+
+int ccka_last_kernel_ms(ccka_ctx* c, double* ms) {
+  if (!c || !ms) return CCKA_EINVAL;
+  if (!c->ran) return fail(c, CCKA_ESTATE, "no rollout yet");
+  *ms = c->last_ms;
+  return CCKA_OK;
+}
+
+int ccka_get_results(ccka_ctx* c, ccka_results* o) {
+  if (!c || !o) return CCKA_EINVAL;
+  if (!c->ran) return fail(c, CCKA_ESTATE, "no rollout yet");
+  (void)hipSetDevice(c->device);
+  const size_t n = (size_t)c->N;
+  const KParams& k = c->kp;
+  struct { void* dst; const void* src; size_t sz; } m[] = {
+      {o->cost_uphmin, k.cost, 8}, {o->energy_wmin, k.energy, 8}, {o->gco2, k.gco2, 8},
+      {o->slo_minutes, k.slo, 4}, {o->pending_pod_minutes, k.pend_min, 8},
+      {o->node_min_spot, k.nmin_spot, 4}, {o->node_min_od, k.nmin_od, 4},
+      {o->launches, k.launches, 4}, {o->deletions, k.deletions, 4}, {o->peak_nodes, k.peak_nodes, 4},
+      {o->final_replicas, k.final_reps, 4}, {o->final_nodes, k.final_nodes, 4},
+      {o->last_choice, k.last_choice, 4}, {o->choice_hash, k.hash, 4}};
+  for (auto& x : m)
+    if (x.dst) HIPCHK(c, hipMemcpyAsync(x.dst, x.src, n * x.sz, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_get_trajectory(ccka_ctx* c, ccka_traj_rec* out, int64_t count) {
+  if (!c || !out) return CCKA_EINVAL;
+  if (!c->traj_valid) return fail(c, CCKA_ESTATE, "last rollout had no trajectory");
+  if (count != c->traj_count) return fail(c, CCKA_EINVAL, "trajectory count mismatch");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(out, c->d_traj, (size_t)count * sizeof(ccka_traj_rec), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_get_totals(ccka_ctx* c, ccka_totals* out) {
+  if (!c || !out) return CCKA_EINVAL;
+  if (!c->ran) return fail(c, CCKA_ESTATE, "no rollout yet");
+  (void)hipSetDevice(c->device);
+  TotParams q{};
+  const KParams& k = c->kp;
+  q.cost = k.cost; q.energy = k.energy; q.gco2 = k.gco2; q.slo = k.slo; q.pend_min = k.pend_min;
+  q.nmin_spot = k.nmin_spot; q.nmin_od = k.nmin_od; q.launches = k.launches; q.deletions = k.deletions;
+  q.parts = (Part*)c->d_parts;
+  q.out = c->d_totals;
+  q.N = c->N;
+  const int nparts = (int)std::min<int64_t>(1024, (c->N + 255) / 256);
+  HIPCHK(c, launch_totals(q, nparts, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_comm_unique_id(uint8_t* id128) {
+  if (!id128) return CCKA_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return CCKA_ERCCL;
+  static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+  std::memcpy(id128, &id, 128);
+  return CCKA_OK;
+}
+
+int ccka_comm_init(ccka_ctx* c, const uint8_t* id128, int32_t nranks, int32_t rank) {
+  if (!c || !id128 || nranks < 1 || rank < 0 || rank >= nranks) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  ncclUniqueId id;
+  std::memcpy(&id, id128, 128);
+  if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+  const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) return fail(c, CCKA_ERCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  return CCKA_OK;
+}
+
+int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
+  if (!c || !io) return CCKA_EINVAL;
+  if (!c->comm) return fail(c, CCKA_ESTATE, "ccka_comm_init first");
+  (void)hipSetDevice(c->device);
+  if (!c->d_totals && hipMalloc((void**)&c->d_totals, sizeof(ccka_totals)) != hipSuccess)
+    return fail(c, CCKA_ENOMEM, "totals alloc");
+  HIPCHK(c, hipMemcpyAsync(c->d_totals, io, sizeof(ccka_totals), hipMemcpyHostToDevice, c->stream));
+  // 8 int64 fields then 2 doubles: one grouped pair of in-place all-reduces
+  ncclGroupStart();
+  ncclResult_t r1 = ncclAllReduce(c->d_totals, c->d_totals, 8, ncclInt64, ncclSum, c->comm, c->stream);
+  ncclResult_t r2 = ncclAllReduce(&c->d_totals->energy_wmin, &c->d_totals->energy_wmin, 2, ncclFloat64,
+                                  ncclSum, c->comm, c->stream);
+  ncclResult_t r3 = ncclGroupEnd();
+  if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
+    return fail(c, CCKA_ERCCL, "ncclAllReduce failed");
+  HIPCHK(c, hipMemcpyAsync(io, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_device_info(ccka_ctx* c, char* name, int32_t name_len, int32_t* cu_count) {
+  if (!c) return CCKA_EINVAL;
+  if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", c->name);
+  if (cu_count) *cu_count = c->cus;
+  return CCKA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,992 @@
+// rollout.hip — MI355X (gfx950) batched policy-rollout engine.
+//
+// One lane = one cluster scenario stepped through the whole horizon
+// (docs/SEMANTICS.md). Decision semantics restate the upstream controllers the
+// reference drives: the peak/off-peak NodePool switch
+// (demo_20_offpeak_configure.sh:59-81, demo_21_peak_configure.sh:56-77,
+// demo_19_reset_policies.sh:68-75), the burst Deployments
+// (demo_30_burst_configure.sh:57-141) and PDB (demo_10_setup_configure.sh:47-56),
+// HPA (k8s 1.34, .env:4), KEDA (.env:10-12), Karpenter 1.8.1 (05_karpenter.sh:20).
+//
+// Data layout in HBM (structure of arrays, coalesced per step):
+//   load[t][d][n]  int32   read once per (step, deployment): 256 B per wave
+//   traj[t][n]     16 B    written once per step (optional): 1 KiB per wave
+//   params/results SoA     read/written once per scenario
+// LDS per workgroup: the catalog (48 B/type), the per-type pod capacity of the
+// single-deployment fast path, the price tile(s) of the current hour for the
+// regions the workgroup covers, and per-wave NodeClaim scratch.
+//
+// Karpenter provisioning is wave-cooperative: lanes that need a NodeClaim are
+// served one after another (ballot), and for each of them all 64 lanes scan a
+// strided slice of the catalog in LDS and reduce with cross-lane shuffles
+// (max-fit and the lexicographic (score, type, zone, cap) argmin).
+//
+// Floating point: binary64, no contraction (pragma below + -ffp-contract=off),
+// operation order identical to the spec, so results are bit-identical to the
+// CPU oracle.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ccka.h"
+#include "kparams.h"
+
+#pragma clang fp contract(off)
+
+namespace ccka {
+
+constexpr int WAVE = 64;
+constexpr int BIGFIT = 0x3fffffff;
+constexpr int CLAIM_FIXED = 7;  // pool, cap, zone, slot, s_cpu, s_mem, s_pods
+
+__device__ __forceinline__ int rdl(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ uint32_t rdlu(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ double rdld(double v, int lane) {
+  long long b = __double_as_longlong(v);
+  int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ long long rdll(long long v, int lane) {
+  int lo = __builtin_amdgcn_readlane((int)(v & 0xffffffffLL), lane);
+  int hi = __builtin_amdgcn_readlane((int)(v >> 32), lane);
+  return ((long long)hi << 32) | (unsigned int)lo;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ void wave_argmin(double& s, int& idx) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double s2 = __shfl_xor(s, o);
+    const int i2 = __shfl_xor(idx, o);
+    if (s2 < s || (s2 == s && i2 < idx)) { s = s2; idx = i2; }
+  }
+}
+__device__ __forceinline__ int capbit(int c) { return c == 0 ? CCKA_CAP_SPOT : CCKA_CAP_OD; }
+
+// ---------------------------------------------------------------------------
+// Philox-4x32-10 and the synthetic load generator (SEMANTICS.md §4)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                       uint32_t k0, uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__global__ void __launch_bounds__(256) gen_load_kernel(GenParams g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int d = blockIdx.y;
+  if (i >= g.n) return;
+  const uint64_t s = (uint64_t)(g.first_id + i);
+  const uint32_t slo = (uint32_t)s, shi = (uint32_t)(s >> 32);
+  const uint32_t k0 = (uint32_t)g.seed, k1 = (uint32_t)(g.seed >> 32);
+  uint32_t u[4], v[4];
+  philox(0xFFFFFFFFu, slo, shi, (uint32_t)d, k0, k1, u);
+  philox(0xFFFFFFFEu, slo, shi, (uint32_t)d, k0, k1, v);
+  const int64_t base = g.base_lo + (int64_t)(u[0] % (uint32_t)(g.base_hi - g.base_lo + 1));
+  const int64_t amp = g.amp_lo + (int64_t)(u[1] % (uint32_t)(g.amp_hi - g.amp_lo + 1));
+  const int phase = (int)(u[2] % 1440u);
+  const bool burst = (int)(u[3] % 1000u) < g.burst_prob;
+  const int bstart = (int)(v[0] % 1440u);
+  for (int t = 0; t < g.T; ++t) {
+    uint32_t e4[4];
+    philox((uint32_t)t, slo, shi, (uint32_t)d, k0, k1, e4);
+    const int64_t e = (int64_t)(e4[0] >> 16) + (int64_t)(e4[1] >> 16) + (int64_t)(e4[2] >> 16) +
+                      (int64_t)(e4[3] >> 16) - 131072;
+    int64_t val = base * (65536000LL + amp * (int64_t)g.sinq[(t + phase) % 1440]) / 65536000LL;
+    val = val * (37837000LL + (int64_t)g.noise * e) / 37837000LL;
+    if (burst && t >= bstart && t < bstart + g.burst_len) val = val * g.burst_mult / 1000;
+    if (val < 0) val = 0;
+    if (val > 0x7fffffff) val = 0x7fffffff;
+    g.out[((int64_t)t * g.D + d) * g.n + i] = (int32_t)val;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Rollout kernel
+// ---------------------------------------------------------------------------
+// node info word: bit0 used | bits1-2 pool | bits3-12 type | bits13-14 zone | bit15 cap
+__device__ __forceinline__ int ni_used(uint32_t x) { return x & 1u; }
+__device__ __forceinline__ int ni_pool(uint32_t x) { return (x >> 1) & 3u; }
+__device__ __forceinline__ int ni_type(uint32_t x) { return (x >> 3) & 1023u; }
+__device__ __forceinline__ int ni_zone(uint32_t x) { return (x >> 13) & 3u; }
+__device__ __forceinline__ int ni_cap(uint32_t x) { return (x >> 15) & 1u; }
+__device__ __forceinline__ uint32_t ni_make(int pool, int type, int zone, int cap) {
+  return 1u | (uint32_t)pool << 1 | (uint32_t)type << 3 | (uint32_t)zone << 13 | (uint32_t)cap << 15;
+}
+
+struct Lds {
+  ccka_itype* types;   // [K]
+  int* cap1;           // [K] pod capacity of deployment 0 from empty (D == 1 path)
+  int* tile;           // [span][K][Z][2]
+  int* claims;         // [waves][MAXN][CLAIM_FIXED + DMAX]
+  int K, Z, rmin;
+};
+
+__device__ __forceinline__ int tprice(const Lds& L, int rl, int k, int z, int c) {
+  return L.tile[((rl * L.K + k) * L.Z + z) * 2 + c];
+}
+
+// largest pod count of deployment d that fits on type k given sums; -1 if the
+// type cannot hold the sums. (SEMANTICS §3.E fit rule)
+template <int DMAX>
+__device__ __forceinline__ int type_fit(const Lds& L, const KParams& p, int k, int s_cpu, int s_mem,
+                                        int s_pods, int d) {
+  if (DMAX == 1) {
+    const int c = L.cap1[k];
+    return c >= s_pods ? c - s_pods : -1;  // exact: floor((A - p*r)/r) = floor(A/r) - p
+  }
+  const ccka_itype& ty = L.types[k];
+  if (s_cpu > ty.alloc_cpu_m || s_mem > ty.alloc_mem_mi || s_pods > ty.max_pods) return -1;
+  int f = ty.max_pods - s_pods;
+  const int rc = p.w->deploy[d].req_cpu_m, rm = p.w->deploy[d].req_mem_mi;
+  if (rc > 0) f = min(f, (ty.alloc_cpu_m - s_cpu) / rc);
+  if (rm > 0) f = min(f, (ty.alloc_mem_mi - s_mem) / rm);
+  return f;
+}
+
+template <int DMAX>
+__device__ __forceinline__ bool type_holds(const Lds& L, int k, int s_cpu, int s_mem, int s_pods) {
+  if (DMAX == 1) return L.cap1[k] >= s_pods;
+  const ccka_itype& ty = L.types[k];
+  return s_cpu <= ty.alloc_cpu_m && s_mem <= ty.alloc_mem_mi && s_pods <= ty.max_pods;
+}
+
+__device__ __forceinline__ bool type_offered(const Lds& L, int rl, int k, uint32_t zm, uint32_t cm) {
+  for (int z = 0; z < L.Z; ++z) {
+    if (!(zm >> z & 1u)) continue;
+    if ((cm & CCKA_CAP_SPOT) && tprice(L, rl, k, z, 0) > 0) return true;
+    if ((cm & CCKA_CAP_OD) && tprice(L, rl, k, z, 1) > 0) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool limit_ok(const Lds& L, int k, int use, int limit) {
+  return limit < 0 || use + L.types[k].vcpu * 1000 <= limit;
+}
+
+// wave-cooperative j (max additional pods of d over candidate types). All
+// arguments are wave-uniform.
+template <int DMAX>
+__device__ int wave_claim_j(const Lds& L, const KParams& p, int rl, uint32_t zm, uint32_t cm,
+                            int s_cpu, int s_mem, int s_pods, int d, int use, int limit, int lane) {
+  int best = 0;
+  for (int k = lane; k < L.K; k += WAVE) {
+    if (!limit_ok(L, k, use, limit)) continue;
+    const int f = type_fit<DMAX>(L, p, k, s_cpu, s_mem, s_pods, d);
+    if (f <= best) continue;
+    if (!type_offered(L, rl, k, zm, cm)) continue;
+    best = f;
+  }
+  return wave_max(best);
+}
+
+// wave-cooperative launch decision; returns packed idx (k*Z+z)*2+c or -1.
+template <int DMAX>
+__device__ int wave_launch(const Lds& L, int rl, uint32_t zm, uint32_t cm, int s_cpu, int s_mem,
+                           int s_pods, int use, int limit, double wc1000, double ci_gpwh, int lane) {
+  bool spot_only = false;
+  if (cm & CCKA_CAP_SPOT) {
+    bool any = false;
+    for (int k = lane; k < L.K && !any; k += WAVE) {
+      if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, use, limit)) continue;
+      for (int z = 0; z < L.Z; ++z)
+        if ((zm >> z & 1u) && tprice(L, rl, k, z, 0) > 0) { any = true; break; }
+    }
+    spot_only = __ballot(any) != 0;
+  }
+  double bs = __builtin_inf();
+  int bi = 0x7fffffff;
+  for (int k = lane; k < L.K; k += WAVE) {
+    if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, use, limit)) continue;
+    const double carbon = L.types[k].p_ref_w * ci_gpwh;
+    for (int z = 0; z < L.Z; ++z) {
+      if (!(zm >> z & 1u)) continue;
+      for (int c = 0; c < 2; ++c) {
+        if (!(cm & (uint32_t)capbit(c))) continue;
+        if (spot_only && c != 0) continue;
+        const int pr = tprice(L, rl, k, z, c);
+        if (pr <= 0) continue;
+        const double score = (double)pr + wc1000 * carbon;
+        if (score < bs) { bs = score; bi = (k * L.Z + z) * 2 + c; }
+      }
+    }
+  }
+  wave_argmin(bs, bi);
+  return bi == 0x7fffffff ? -1 : bi;
+}
+
+template <int DMAX, int MAXN>
+__global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const ccka_world* __restrict__ w = p.w;
+  const int K = p.K, Z = p.Z, D = p.D, NP = p.P, NN = p.maxn;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+  const bool active = i < p.N;
+
+  Lds L;
+  L.K = K;
+  L.Z = Z;
+  L.types = reinterpret_cast<ccka_itype*>(smem);
+  L.cap1 = reinterpret_cast<int*>(smem + p.lds_off_cap1);
+  L.tile = reinterpret_cast<int*>(smem + p.lds_off_tile);
+  L.claims = reinterpret_cast<int*>(smem + p.lds_off_claims) + wid * MAXN * (CLAIM_FIXED + DMAX);
+  int* s_rng = reinterpret_cast<int*>(smem + p.lds_off_misc);
+
+  // ---- stage the catalog, the region range of this block ----
+  for (int k = tid; k < K; k += blockDim.x) {
+    const ccka_itype ty = p.types[k];
+    L.types[k] = ty;
+    if (DMAX == 1) {
+      const int rc = w->deploy[0].req_cpu_m, rm = w->deploy[0].req_mem_mi;
+      int f = ty.max_pods;
+      if (rc > 0) f = min(f, ty.alloc_cpu_m / rc);
+      if (rm > 0) f = min(f, ty.alloc_mem_mi / rm);
+      L.cap1[k] = f;
+    }
+  }
+  const int my_r = active ? (p.region ? (int)p.region[i] : 0) : 0x7fffffff;
+  if (tid == 0) { s_rng[0] = 0x7fffffff; }
+  __syncthreads();
+  if (active) atomicMin(&s_rng[0], my_r);
+  __syncthreads();
+  L.rmin = s_rng[0] == 0x7fffffff ? 0 : s_rng[0];
+  const int rl = active ? my_r - L.rmin : 0;
+  const int tile_ints = K * Z * 2;
+
+  // ---- per-scenario parameters ----
+  const double cw = active && p.cw ? p.cw[i] : w->carbon_weight;
+  const double wc1000 = cw * 1000.0;
+  const int reset_ca = active && p.reset_ca ? (int)p.reset_ca[i] : w->reset_ca_s;
+  const int pswitch = active && p.pswitch ? (int)p.pswitch[i] : w->peak_switch;
+
+  int target[DMAX], maxr[DMAX], dstab[DMAX];
+  uint32_t capsel[DMAX];
+  int replicas[DMAX], last_active[DMAX];
+  int rec[DMAX][CCKA_HIST], delta[DMAX][CCKA_HIST];
+  uint32_t recv[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    const ccka_deployment& dp = w->deploy[d < D ? d : 0];
+    target[d] = dp.target_util_pct;
+    maxr[d] = dp.max_replicas;
+    dstab[d] = dp.down.stab_window_s;
+    if (active && dp.scaler == CCKA_SCALER_HPA) {
+      if (p.target) target[d] = p.target[i];
+      if (p.maxr) maxr[d] = p.maxr[i];
+      if (p.down_stab) dstab[d] = p.down_stab[i];
+    }
+    capsel[d] = active && p.cap_sel ? (uint32_t)p.cap_sel[i] : dp.cap_sel;
+    replicas[d] = dp.replicas0;
+    last_active[d] = 0;
+    recv[d] = 0;
+#pragma unroll
+    for (int k = 0; k < CCKA_HIST; ++k) { rec[d][k] = 0; delta[d][k] = 0; }
+  }
+  // pools: policy | ca_s, zone, cap
+  int ppol[CCKA_MAX_POOLS], pca[CCKA_MAX_POOLS];
+  uint32_t pzm[CCKA_MAX_POOLS], pcm[CCKA_MAX_POOLS];
+#pragma unroll
+  for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
+    ppol[q] = 0; pca[q] = 0; pzm[q] = 0; pcm[q] = 0;
+    if (q < NP) {
+      const ccka_pool& pl = w->pools[q];
+      const ccka_pool_patch* pp[2] = {&pl.base, &pl.profile[CCKA_PROFILE_RESET]};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const ccka_pool_patch& x = *pp[s];
+        if (x.policy != CCKA_POLICY_KEEP) ppol[q] = x.policy;
+        if (x.consolidate_after_s >= 0) pca[q] = s == 1 ? reset_ca : x.consolidate_after_s;
+        if (x.zone_mask) pzm[q] = x.zone_mask;
+        if (x.cap_mask) pcm[q] = x.cap_mask;
+      }
+    }
+  }
+  uint32_t ninfo[MAXN];
+  int nready[MAXN], nlast[MAXN];
+  int npods[MAXN][DMAX];
+#pragma unroll
+  for (int n = 0; n < MAXN; ++n) {
+    ninfo[n] = 0; nready[n] = 0; nlast[n] = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
+  }
+  int profile = -1;
+  long long cost = 0, pend_min = 0, burn = 0, base_price = 0;
+  double energy = 0.0, gco2 = 0.0, ci_gpwmin = 0.0, ci_gpwh = 0.0;
+  int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
+  uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
+  const ccka_itype bt = p.types[w->base_type];
+  const double base_w = (double)w->base_nodes * (bt.p_idle_w + bt.p_dyn_w * w->base_util);
+  const int ps = w->peak_start_min, pe = w->peak_end_min;
+
+  int hour = -1;
+  for (int t = 0; t < p.T; ++t) {
+    const int minute = (w->start_minute + t) % 1440;
+    const int h = minute / 60;
+    if (h != hour) {  // block-uniform: stage this hour's price tiles
+      hour = h;
+      __syncthreads();
+      for (int rr = 0; rr < p.span; ++rr) {
+        const int rg = L.rmin + rr;
+        if (rg >= p.R) break;
+        const int* src = p.price + ((int64_t)rg * 24 + h) * tile_ints;
+        for (int x = tid; x < tile_ints; x += blockDim.x) L.tile[rr * tile_ints + x] = src[x];
+      }
+      __syncthreads();
+      if (active) {
+        ci_gpwmin = p.ci_gpwmin[my_r * 24 + h];
+        ci_gpwh = p.ci_gpwh[my_r * 24 + h];
+        base_price = (long long)w->base_nodes * tprice(L, rl, w->base_type, 0, 1);
+        burn = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n)
+          if (ni_used(ninfo[n]))
+            burn += tprice(L, rl, ni_type(ninfo[n]), ni_zone(ninfo[n]), ni_cap(ninfo[n]));
+      }
+    }
+    uint32_t flags = 0;
+    int step_last_type = 0xFFFF;
+    int util_valid[DMAX], util[DMAX], Lt[DMAX], pend[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; Lt[d] = 0; pend[d] = 0; }
+
+    if (active) {
+      // ---- A. profile ----
+      const bool in_win = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
+      const bool peak = pswitch && in_win;
+      const int prof = peak ? CCKA_PROFILE_PEAK : CCKA_PROFILE_OFFPEAK;
+      if (peak) flags |= 1u;
+      if (prof != profile) {
+        profile = prof;
+#pragma unroll
+        for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
+          if (q >= NP) break;
+          const ccka_pool_patch& x = w->pools[q].profile[prof];
+          if (x.policy != CCKA_POLICY_KEEP) ppol[q] = x.policy;
+          if (x.consolidate_after_s >= 0) pca[q] = x.consolidate_after_s;
+          if (x.zone_mask) pzm[q] = x.zone_mask;
+          if (x.cap_mask) pcm[q] = x.cap_mask;
+        }
+      }
+      // ---- C. scalers ----
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d >= D) break;
+        const ccka_deployment& dp = w->deploy[d];
+        const int Lv = p.load[((int64_t)t * D + d) * p.N + i];
+        Lt[d] = Lv;
+        if (dp.scaler == CCKA_SCALER_STATIC) continue;
+        int ready = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n)
+          if (ni_used(ninfo[n]) && nready[n] <= t) ready += npods[n][d];
+        const int cur = replicas[d];
+        int desired = cur, proposal = cur;
+        bool ran = false, hpa_path = false;
+        int minr = dp.min_replicas, mx = maxr[d];
+        bool do_behavior = false;
+        if (dp.scaler == CCKA_SCALER_HPA) {
+          hpa_path = true;
+          if (cur == 0 && minr != 0) { hpa_path = false; }
+          else if (cur > mx) desired = mx;
+          else if (cur < minr) desired = minr;
+          else if (ready > 0) {
+            long long usage = Lv;
+            if (dp.limit_cpu_m > 0) usage = min(usage, (long long)ready * dp.limit_cpu_m);
+            const int u = (int)((usage * 100) / ((long long)ready * dp.req_cpu_m));
+            util_valid[d] = 1;
+            util[d] = u;
+            const double ratio = (double)u / (double)target[d];
+            const double lo = 1.0 - dp.tolerance, hi = 1.0 + dp.tolerance;
+            if (cur - ready > 0 && ratio > 1.0) {
+              const int nu = (int)((usage * 100) / ((long long)cur * dp.req_cpu_m));
+              const double nr = (double)nu / (double)target[d];
+              if ((lo <= nr && nr <= hi) || nr < 1.0) proposal = cur;
+              else proposal = max(cur, (int)ceil(nr * (double)cur));
+            } else if (lo <= ratio && ratio <= hi) {
+              proposal = cur;
+            } else {
+              proposal = (int)ceil(ratio * (double)ready);
+            }
+            do_behavior = true;
+          }
+        } else {  // KEDA
+          const bool act = (long long)Lv > dp.keda_activation;
+          if (act) last_active[d] = t;
+          if (cur == 0) desired = act ? 1 : 0;
+          else if (!act && dp.keda_min == 0 && (t - last_active[d]) * CCKA_STEP_SECONDS >= dp.keda_cooldown_s)
+            desired = 0;
+          else {
+            hpa_path = true;
+            minr = max(dp.keda_min, 1);
+            mx = dp.keda_max;
+            if (cur > mx) desired = mx;
+            else if (cur < minr) desired = minr;
+            else {
+              const double r = (double)Lv / ((double)dp.keda_threshold * (double)cur);
+              const double lo = 1.0 - dp.tolerance, hi = 1.0 + dp.tolerance;
+              proposal = (lo <= r && r <= hi) ? cur : (int)ceil((double)Lv / (double)dp.keda_threshold);
+              do_behavior = true;
+            }
+          }
+        }
+        if (do_behavior) {
+          ran = true;
+          // stabilisation
+          const int upw = dp.up.stab_window_s, dnw = dstab[d];
+          int upr = proposal, dnr = proposal;
+#pragma unroll
+          for (int k = 0; k < CCKA_HIST; ++k) {
+            if (!(recv[d] >> k & 1u)) continue;
+            const int age = (k + 1) * CCKA_STEP_SECONDS;
+            if (age < upw) upr = min(upr, rec[d][k]);
+            if (age < dnw) dnr = max(dnr, rec[d][k]);
+          }
+          int rc = max(cur, upr);
+          rc = min(rc, dnr);
+          int lo = minr, hi = mx;
+          if (rc > cur) {
+            const ccka_hpa_rules& R = dp.up;
+            int lim = cur;
+            if (R.select != CCKA_SELECT_DISABLED) {
+              long long res = R.select == CCKA_SELECT_MIN ? 0x7fffffffLL : -0x80000000LL;
+              for (int q = 0; q < R.n_policies; ++q) {
+                const ccka_hpa_policy& pol = R.policies[q];
+                int added = 0, removed = 0;
+#pragma unroll
+                for (int k = 0; k < CCKA_HIST; ++k)
+                  if ((k + 1) * CCKA_STEP_SECONDS < pol.period_s) {
+                    added += max(delta[d][k], 0);
+                    removed += max(-delta[d][k], 0);
+                  }
+                const long long pst = (long long)cur - added + removed;
+                long long pr;
+                if (pol.type == CCKA_HPA_PODS) pr = pst + pol.value;
+                else pr = (int)ceil((double)pst * (1.0 + (double)pol.value / 100.0));
+                res = R.select == CCKA_SELECT_MIN ? min(res, pr) : max(res, pr);
+              }
+              lim = (int)res;
+            }
+            lim = max(lim, cur);
+            hi = min(hi, lim);
+          } else if (rc < cur) {
+            const ccka_hpa_rules& R = dp.down;
+            int lim = cur;
+            if (R.select != CCKA_SELECT_DISABLED) {
+              long long res = R.select == CCKA_SELECT_MIN ? -0x80000000LL : 0x7fffffffLL;
+              for (int q = 0; q < R.n_policies; ++q) {
+                const ccka_hpa_policy& pol = R.policies[q];
+                int added = 0, removed = 0;
+#pragma unroll
+                for (int k = 0; k < CCKA_HIST; ++k)
+                  if ((k + 1) * CCKA_STEP_SECONDS < pol.period_s) {
+                    added += max(delta[d][k], 0);
+                    removed += max(-delta[d][k], 0);
+                  }
+                const long long pst = (long long)cur - added + removed;
+                long long pr;
+                if (pol.type == CCKA_HPA_PODS) pr = pst - pol.value;
+                else pr = (int)((double)pst * (1.0 - (double)pol.value / 100.0));
+                res = R.select == CCKA_SELECT_MIN ? max(res, pr) : min(res, pr);
+              }
+              lim = (int)res;
+            }
+            lim = min(lim, cur);
+            lo = max(lo, lim);
+          }
+          desired = rc < lo ? lo : (rc > hi ? hi : rc);
+        }
+        // shift history rings; entry 0 = this step
+#pragma unroll
+        for (int k = CCKA_HIST - 1; k > 0; --k) { rec[d][k] = rec[d][k - 1]; delta[d][k] = delta[d][k - 1]; }
+        rec[d][0] = ran ? proposal : 0;
+        recv[d] = ((recv[d] << 1) | (ran ? 1u : 0u)) & 0xFFu;
+        delta[d][0] = (hpa_path && desired != cur) ? desired - cur : 0;
+        replicas[d] = desired;
+      }
+      // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d >= D) break;
+        int total = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) total += ni_used(ninfo[n]) ? npods[n][d] : 0;
+        int excess = total - replicas[d];
+        if (excess > 0) {
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+            for (int n = MAXN - 1; n >= 0; --n) {
+              const bool rdy = nready[n] <= t;
+              if (ni_used(ninfo[n]) && rdy == (pass == 1) && npods[n][d] > 0 && excess > 0) {
+                const int k = min(npods[n][d], excess);
+                npods[n][d] -= k;
+                excess -= k;
+                nlast[n] = t;
+              }
+            }
+          }
+        }
+      }
+      // ---- E. kube-scheduler (ready) / F1. nomination (in-flight) ----
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          if (d >= D) break;
+          int total = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) total += ni_used(ninfo[n]) ? npods[n][d] : 0;
+          int pd = replicas[d] - total;
+          if (pd > 0) {
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              const uint32_t x = ninfo[n];
+              const bool rdy = nready[n] <= t;
+              if (pd > 0 && ni_used(x) && rdy == (pass == 0) && (capbit(ni_cap(x)) & capsel[d])) {
+                int sc = 0, sm = 0, sp = 0;
+#pragma unroll
+                for (int e = 0; e < DMAX; ++e) {
+                  if (e >= D) break;
+                  sc += npods[n][e] * w->deploy[e].req_cpu_m;
+                  sm += npods[n][e] * w->deploy[e].req_mem_mi;
+                  sp += npods[n][e];
+                }
+                const int f = max(type_fit<DMAX>(L, p, ni_type(x), sc, sm, sp, d), 0);
+                const int k = min(f, pd);
+                if (k > 0) { npods[n][d] += k; pd -= k; nlast[n] = t; }
+              }
+            }
+          }
+          pend[d] = pd;
+        }
+      }
+    }
+
+    // ---- F2. Karpenter provisioning, wave-cooperative ----
+    {
+      int anyp = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) anyp |= pend[d] > 0;
+      uint32_t free_mask = 0;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) if (!ni_used(ninfo[n]) && n < NN) free_mask |= 1u << n;
+      unsigned long long need = __ballot(active && anyp && free_mask != 0);
+      while (need) {
+        const int ld = __ffsll((long long)need) - 1;
+        need &= need - 1;
+        // broadcast the leader's state
+        const int lrl = rdl(rl, ld);
+        const double lwc = rdld(wc1000, ld);
+        const double lci = rdld(ci_gpwh, ld);
+        uint32_t lfree = rdlu(free_mask, ld);
+        int use0[CCKA_MAX_POOLS], usenow[CCKA_MAX_POOLS];
+        uint32_t lzm[CCKA_MAX_POOLS], lcm[CCKA_MAX_POOLS];
+#pragma unroll
+        for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
+          int u = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n)
+            if (ni_used(ninfo[n]) && ni_pool(ninfo[n]) == q) u += L.types[ni_type(ninfo[n])].vcpu * 1000;
+          use0[q] = rdl(u, ld);
+          usenow[q] = use0[q];
+          lzm[q] = rdlu(pzm[q], ld);
+          lcm[q] = rdlu(pcm[q], ld);
+        }
+        int* CL = L.claims;
+        const int CW = CLAIM_FIXED + DMAX;
+        int ncl = 0;
+        for (int oi = 0; oi < D; ++oi) {
+          const int d = p.prov[oi];
+          int pd_self = 0;
+#pragma unroll
+          for (int e = 0; e < DMAX; ++e) if (e == d) pd_self = pend[e];
+          int rem = rdl(pd_self, ld);
+          if (rem <= 0) continue;
+          uint32_t csel_self = 0;
+#pragma unroll
+          for (int e = 0; e < DMAX; ++e) if (e == d) csel_self = capsel[e];
+          const uint32_t csel = rdlu(csel_self, ld);
+          const int rc = w->deploy[d].req_cpu_m, rm = w->deploy[d].req_mem_mi;
+          for (int c = 0; c < ncl && rem > 0; ++c) {
+            int* cl = CL + c * CW;
+            const int cpool = cl[0];
+            const uint32_t cm = (uint32_t)cl[1] & csel;
+            if (!cm) continue;
+            const int j = wave_claim_j<DMAX>(L, p, lrl, (uint32_t)cl[2], cm, cl[4], cl[5], cl[6], d,
+                                             use0[cpool], w->pools[cpool].limit_cpu_m, lane);
+            if (j <= 0) continue;
+            const int k = min(j, rem);
+            __builtin_amdgcn_wave_barrier();
+            cl[1] = (int)cm;
+            cl[4] += k * rc;
+            cl[5] += k * rm;
+            cl[6] += k;
+            cl[CLAIM_FIXED + d] += k;
+            __builtin_amdgcn_wave_barrier();
+            rem -= k;
+          }
+          while (rem > 0 && lfree) {
+            const int slot = __ffs((int)lfree) - 1;
+            int chosen = -1, jj = 0;
+            for (int q = 0; q < NP; ++q) {
+              const uint32_t cm = lcm[q] & csel;
+              if (!cm) continue;
+              const int j = wave_claim_j<DMAX>(L, p, lrl, lzm[q], cm, 0, 0, 0, d, use0[q],
+                                               w->pools[q].limit_cpu_m, lane);
+              if (j > 0) { chosen = q; jj = j; break; }
+            }
+            if (chosen < 0) break;
+            const int k = min(jj, rem);
+            int* cl = CL + ncl * CW;
+            __builtin_amdgcn_wave_barrier();
+            cl[0] = chosen;
+            cl[1] = (int)(lcm[chosen] & csel);
+            cl[2] = (int)lzm[chosen];
+            cl[3] = slot;
+            cl[4] = k * rc;
+            cl[5] = k * rm;
+            cl[6] = k;
+            for (int e = 0; e < DMAX; ++e) cl[CLAIM_FIXED + e] = e == d ? k : 0;
+            __builtin_amdgcn_wave_barrier();
+            ncl++;
+            lfree &= ~(1u << slot);
+            rem -= k;
+          }
+        }
+        // launch in creation order
+        for (int c = 0; c < ncl; ++c) {
+          const int* cl = CL + c * CW;
+          const int cpool = cl[0];
+          const int bi = wave_launch<DMAX>(L, lrl, (uint32_t)cl[2], (uint32_t)cl[1], cl[4], cl[5],
+                                           cl[6], usenow[cpool], w->pools[cpool].limit_cpu_m, lwc,
+                                           lci, lane);
+          if (bi < 0) continue;
+          const int bc = bi & 1, bz = (bi >> 1) % Z, bk = (bi >> 1) / Z;
+          usenow[cpool] += L.types[bk].vcpu * 1000;
+          const int slot = cl[3];
+          if (lane == ld) {
+            const uint32_t choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)cpool << 16;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (n == slot) {
+                ninfo[n] = ni_make(cpool, bk, bz, bc);
+                nready[n] = t + w->provision_delay_steps;
+                nlast[n] = t;
+#pragma unroll
+                for (int e = 0; e < DMAX; ++e) npods[n][e] = e < D ? cl[CLAIM_FIXED + e] : 0;
+              }
+            }
+            burn += tprice(L, lrl, bk, bz, bc);
+            launches++;
+            last_choice = choice;
+            hash = (hash ^ choice) * 16777619u;
+            step_last_type = bk;
+            flags |= 2u;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+
+    if (active) {
+      // ---- G. disruption ----
+      long long allowed = 0x3fffffffffffffffLL;
+      if (w->pdb_min_available_pct >= 0) {
+        long long rdy = 0, reps = 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          if (d >= D || !w->deploy[d].pdb_member) continue;
+          reps += replicas[d];
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n)
+            if (ni_used(ninfo[n]) && nready[n] <= t) rdy += npods[n][d];
+        }
+        allowed = max(rdy - ((long long)w->pdb_min_available_pct * reps + 99) / 100, 0LL);
+      }
+      for (int q = 0; q < NP; ++q) {
+        int npool = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) npool += (ni_used(ninfo[n]) && ni_pool(ninfo[n]) == q) ? 1 : 0;
+        if (npool == 0) continue;
+        const int budget = (w->pools[q].budget_pct * npool + 99) / 100;
+        int deleted = 0;
+        uint32_t rejected = 0;
+        while (deleted < budget) {
+          int best = -1, bpods = 0, bprice = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            const uint32_t x = ninfo[n];
+            if (!ni_used(x) || ni_pool(x) != q || nready[n] > t || (rejected >> n & 1u)) continue;
+            if ((t - nlast[n]) * CCKA_STEP_SECONDS < pca[q]) continue;
+            int pods = 0;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n][d] : 0;
+            if (pods > 0 && ppol[q] != CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) continue;
+            const int pr = tprice(L, rl, ni_type(x), ni_zone(x), ni_cap(x));
+            if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
+          }
+          if (best < 0) break;
+          bool ok = true;
+          long long pdb_pods = 0;
+          int tpods[MAXN][DMAX];
+          int tlast[MAXN];
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            tlast[n] = nlast[n];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) tpods[n][d] = npods[n][d];
+          }
+          if (bpods > 0) {
+            int bp[DMAX];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) {
+              bp[d] = 0;
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) if (n == best) bp[d] = npods[n][d];
+              if (d < D && w->deploy[d].pdb_member) pdb_pods += bp[d];
+            }
+            if (pdb_pods > allowed) ok = false;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) {
+              if (d >= D || !ok) break;
+              int need_d = bp[d];
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                const uint32_t x = ninfo[n];
+                if (need_d > 0 && n != best && ni_used(x) && nready[n] <= t && (capbit(ni_cap(x)) & capsel[d])) {
+                  int sc = 0, sm = 0, sp = 0;
+#pragma unroll
+                  for (int e = 0; e < DMAX; ++e) {
+                    if (e >= D) break;
+                    sc += tpods[n][e] * w->deploy[e].req_cpu_m;
+                    sm += tpods[n][e] * w->deploy[e].req_mem_mi;
+                    sp += tpods[n][e];
+                  }
+                  const int f = max(type_fit<DMAX>(L, p, ni_type(x), sc, sm, sp, d), 0);
+                  const int k = min(f, need_d);
+                  if (k > 0) { tpods[n][d] += k; need_d -= k; tlast[n] = t; }
+                }
+              }
+              if (need_d > 0) ok = false;
+            }
+          }
+          if (!ok) { rejected |= 1u << best; continue; }
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            nlast[n] = tlast[n];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) npods[n][d] = tpods[n][d];
+            if (n == best) {
+              burn -= bprice;
+              ninfo[n] = 0; nready[n] = 0; nlast[n] = 0;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
+            }
+          }
+          allowed -= pdb_pods;
+          deleted++;
+          deletions++;
+          flags |= 4u;
+        }
+      }
+      // ---- H. accounting ----
+      int ready_d[DMAX];
+      double upp[DMAX];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        ready_d[d] = 0;
+        upp[d] = 0.0;
+        if (d >= D) continue;
+        int rd = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) if (ni_used(ninfo[n]) && nready[n] <= t) rd += npods[n][d];
+        ready_d[d] = rd;
+        if (rd > 0) {
+          long long usage = Lt[d];
+          if (w->deploy[d].limit_cpu_m > 0) usage = min(usage, (long long)rd * w->deploy[d].limit_cpu_m);
+          upp[d] = (double)usage / (double)rd;
+        }
+      }
+      double step_w = base_w;
+      int nsp = 0, nod = 0;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const uint32_t x = ninfo[n];
+        if (!ni_used(x)) continue;
+        const ccka_itype& ty = L.types[ni_type(x)];
+        double u = 0.0;
+        if (nready[n] <= t) {
+          double xs = 0.0;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) if (d < D) xs += (double)npods[n][d] * upp[d];
+          u = xs * ty.inv_alloc_cpu;
+          if (u > 1.0) u = 1.0;
+        }
+        step_w += ty.p_idle_w + ty.p_dyn_w * u;
+        if (ni_cap(x) == 0) nsp++; else nod++;
+      }
+      cost += burn + base_price;
+      energy += step_w;
+      gco2 += step_w * ci_gpwmin;
+      int pending = 0, reps = 0;
+      bool viol = false;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        if (d >= D) continue;
+        pending += replicas[d] - ready_d[d];
+        reps += replicas[d];
+        const ccka_deployment& dp = w->deploy[d];
+        if (dp.scaler == CCKA_SCALER_HPA && util_valid[d] && util[d] > w->slo_util_pct) viol = true;
+        if (dp.scaler == CCKA_SCALER_KEDA && (long long)Lt[d] > dp.keda_activation && replicas[d] == 0) viol = true;
+      }
+      if (pending > 0) viol = true;
+      if (viol) { slo++; flags |= 8u; }
+      pend_min += pending;
+      nmin_spot += nsp;
+      nmin_od += nod;
+      peak_nodes = max(peak_nodes, nsp + nod);
+      if (p.traj) {
+        ccka_traj_rec rcd;
+        rcd.replicas = reps;
+        rcd.pending = pending;
+        rcd.nodes_spot = (uint16_t)nsp;
+        rcd.nodes_od = (uint16_t)nod;
+        rcd.last_type = (uint16_t)step_last_type;
+        rcd.flags = (uint16_t)flags;
+        *reinterpret_cast<int4*>(&p.traj[(int64_t)t * p.N + i]) = *reinterpret_cast<int4*>(&rcd);
+      }
+    }
+  }
+  if (!active) return;
+  int reps = 0, nodes = 0;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) reps += d < D ? replicas[d] : 0;
+#pragma unroll
+  for (int n = 0; n < MAXN; ++n) nodes += ni_used(ninfo[n]);
+  p.cost[i] = cost;
+  p.energy[i] = energy;
+  p.gco2[i] = gco2;
+  p.slo[i] = slo;
+  p.pend_min[i] = pend_min;
+  p.nmin_spot[i] = nmin_spot;
+  p.nmin_od[i] = nmin_od;
+  p.launches[i] = launches;
+  p.deletions[i] = deletions;
+  p.peak_nodes[i] = peak_nodes;
+  p.final_reps[i] = reps;
+  p.final_nodes[i] = nodes;
+  p.last_choice[i] = last_choice;
+  p.hash[i] = hash;
+}
+
+// ---------------------------------------------------------------------------
+// Totals: fixed-order block partials, then one ordered final pass.
+// ---------------------------------------------------------------------------
+struct Part {
+  long long v[8];
+  double e, g;
+};
+
+__global__ void __launch_bounds__(256) totals_partial(TotParams q) {
+  __shared__ Part sp[256];
+  const int tid = threadIdx.x;
+  Part a;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a.v[k] = 0;
+  a.e = 0.0;
+  a.g = 0.0;
+  const int64_t chunk = (q.N + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(lo + chunk, q.N);
+  for (int64_t i = lo + tid; i < hi; i += blockDim.x) {
+    a.v[0] += 1;
+    a.v[1] += q.cost[i];
+    a.v[2] += q.slo[i];
+    a.v[3] += q.pend_min[i];
+    a.v[4] += q.nmin_spot[i];
+    a.v[5] += q.nmin_od[i];
+    a.v[6] += q.launches[i];
+    a.v[7] += q.deletions[i];
+    a.e += q.energy[i];
+    a.g += q.gco2[i];
+  }
+  sp[tid] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sp[tid].v[k] += sp[tid + s].v[k];
+      sp[tid].e += sp[tid + s].e;
+      sp[tid].g += sp[tid + s].g;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) q.parts[blockIdx.x] = sp[0];
+}
+
+__global__ void totals_final(TotParams q, int nparts) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Part a;
+  for (int k = 0; k < 8; ++k) a.v[k] = 0;
+  a.e = 0.0;
+  a.g = 0.0;
+  for (int b = 0; b < nparts; ++b) {
+    for (int k = 0; k < 8; ++k) a.v[k] += q.parts[b].v[k];
+    a.e += q.parts[b].e;
+    a.g += q.parts[b].g;
+  }
+  ccka_totals* o = q.out;
+  o->scenarios = a.v[0];
+  o->cost_uphmin = a.v[1];
+  o->slo_minutes = a.v[2];
+  o->pending_pod_minutes = a.v[3];
+  o->node_min_spot = a.v[4];
+  o->node_min_od = a.v[5];
+  o->launches = a.v[6];
+  o->deletions = a.v[7];
+  o->energy_wmin = a.e;
+  o->gco2 = a.g;
+}
+
+// ---------------------------------------------------------------------------
+// launchers (called from ccka_abi.cpp)
+// ---------------------------------------------------------------------------
+hipError_t launch_gen_load(const GenParams& g, hipStream_t s) {
+  dim3 grid((unsigned)((g.n + 255) / 256), (unsigned)g.D);
+  hipLaunchKernelGGL(gen_load_kernel, grid, dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s) {
+  const unsigned grid = (unsigned)((p.N + block - 1) / block);
+  if (p.D == 1 && p.maxn <= 8)
+    hipLaunchKernelGGL((rollout_kernel<1, 8>), dim3(grid), dim3(block), lds, s, p);
+  else if (p.D == 1)
+    hipLaunchKernelGGL((rollout_kernel<1, 16>), dim3(grid), dim3(block), lds, s, p);
+  else if (p.D <= 4)
+    hipLaunchKernelGGL((rollout_kernel<4, 16>), dim3(grid), dim3(block), lds, s, p);
+  else
+    hipLaunchKernelGGL((rollout_kernel<16, 16>), dim3(grid), dim3(block), lds, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_totals(const TotParams& q, int nparts, hipStream_t s) {
+  hipLaunchKernelGGL(totals_partial, dim3(nparts), dim3(256), 0, s, q);
+  hipLaunchKernelGGL(totals_final, dim3(1), dim3(64), 0, s, q, nparts);
+  return hipGetLastError();
+}
+
+}  // namespace ccka

@@ -1,0 +1,284 @@
+/*
+ * ccka.h — C ABI of the MI355X policy-rollout engine (libccka.so).
+ *
+ * Drop-in boundary for the reference's decision path. In the reference the
+ * decision path is reached through Kubernetes objects: `kubectl patch
+ * nodepool` merge patches on spec.disruption
+ * (demo_20_offpeak_configure.sh:59-60, demo_21_peak_configure.sh:56-57,
+ * demo_19_reset_policies.sh:68-75), RFC 6902 patches on
+ * /spec/template/spec/requirements (demo_20_offpeak_configure.sh:64-81,96;
+ * demo_21_peak_configure.sh:60-77,88) and `kubectl apply` of the burst
+ * Deployments and PDB (demo_30_burst_configure.sh:78-143,
+ * demo_10_setup_configure.sh:47-56), reconciled by upstream HPA/KEDA/Karpenter.
+ * Here those objects are ingested by the host (ccka_host.h) into the POD
+ * structs below and the decisions for millions of independent cluster
+ * scenarios are evaluated on the GPU. Semantics: docs/SEMANTICS.md.
+ *
+ * Conventions: plain C, explicit widths, no allocation escapes the ABI.
+ * The caller owns every host buffer; the library owns device buffers inside
+ * the context. Calls are blocking (stream-synchronous at return) unless the
+ * name ends in _async. One context per device and per host thread.
+ * Return 0 on success or a negative ccka_status; message via ccka_last_error.
+ */
+#ifndef CCKA_H
+#define CCKA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCKA_ABI_VERSION 1
+
+#define CCKA_STEP_SECONDS 60
+#define CCKA_MAX_TYPES 1024
+#define CCKA_MAX_ZONES 4
+#define CCKA_MAX_REGIONS 16
+#define CCKA_MAX_POOLS 4
+#define CCKA_MAX_DEPLOY 16
+#define CCKA_MAX_NODES 16
+#define CCKA_HIST 8              /* history ring depth (steps) for HPA windows */
+#define CCKA_HOURS 24
+
+enum ccka_status {
+  CCKA_OK = 0,
+  CCKA_EINVAL = -1,   /* invalid argument / world fails validation */
+  CCKA_ENOMEM = -2,   /* device or host allocation failed */
+  CCKA_EHIP = -3,     /* HIP runtime error */
+  CCKA_ERCCL = -4,    /* RCCL error */
+  CCKA_EPARITY = -5,  /* self-check mismatch */
+  CCKA_ESTATE = -6,   /* call order (e.g. rollout before set_world) */
+  CCKA_ENODEV = -7    /* no usable gfx950 device */
+};
+
+/* capacity-type bits (karpenter.sh/capacity-type); offering index c: 0 spot, 1 on-demand */
+enum { CCKA_CAP_SPOT = 1, CCKA_CAP_OD = 2 };
+/* NodePool spec.disruption.consolidationPolicy */
+enum { CCKA_POLICY_KEEP = 0, CCKA_WHEN_EMPTY = 1, CCKA_WHEN_EMPTY_OR_UNDERUTILIZED = 2 };
+enum { CCKA_SCALER_STATIC = 0, CCKA_SCALER_HPA = 1, CCKA_SCALER_KEDA = 2 };
+enum { CCKA_PROFILE_RESET = 0, CCKA_PROFILE_OFFPEAK = 1, CCKA_PROFILE_PEAK = 2 };
+/* HPA behavior */
+enum { CCKA_SELECT_MAX = 0, CCKA_SELECT_MIN = 1, CCKA_SELECT_DISABLED = 2 };
+enum { CCKA_HPA_PODS = 1, CCKA_HPA_PERCENT = 2 };
+
+/* One EC2 instance type of the catalog (the ~800-entry catalog Karpenter's AWS
+ * provider discovers at runtime, 05_karpenter.sh:64-75). Doubles are
+ * precomputed by the host from the power model. 48 bytes. */
+typedef struct ccka_itype {
+  int32_t vcpu;
+  int32_t alloc_cpu_m;    /* allocatable millicores (after kube-reserved)   */
+  int32_t alloc_mem_mi;   /* allocatable MiB                                */
+  int32_t max_pods;
+  double p_idle_w;        /* vcpu*Wmin*PUE                                  */
+  double p_dyn_w;         /* vcpu*(Wmax-Wmin)*PUE                           */
+  double p_ref_w;         /* p_idle_w + 0.5*p_dyn_w (launch-score power)    */
+  double inv_alloc_cpu;   /* 1.0/alloc_cpu_m                                */
+} ccka_itype;
+
+/* A NodePool patch profile (merge semantics: 0 / -1 = keep). */
+typedef struct ccka_pool_patch {
+  int32_t policy;               /* CCKA_POLICY_*                     */
+  int32_t consolidate_after_s;  /* -1 keep                           */
+  uint32_t zone_mask;           /* topology.kubernetes.io/zone In .. */
+  uint32_t cap_mask;            /* karpenter.sh/capacity-type In ..  */
+} ccka_pool_patch;
+
+typedef struct ccka_pool {
+  int32_t limit_cpu_m;          /* spec.limits.cpu in millicores, -1 none */
+  int32_t budget_pct;           /* disruption budget nodes %, default 10  */
+  ccka_pool_patch base;         /* the NodePool as created                */
+  ccka_pool_patch profile[3];   /* RESET, OFFPEAK, PEAK                   */
+} ccka_pool;
+
+typedef struct ccka_hpa_policy {
+  int32_t type;       /* CCKA_HPA_PODS / CCKA_HPA_PERCENT */
+  int32_t value;
+  int32_t period_s;   /* <= 480 */
+} ccka_hpa_policy;
+
+typedef struct ccka_hpa_rules {
+  int32_t select;       /* CCKA_SELECT_* */
+  int32_t n_policies;   /* 0..2 */
+  int32_t stab_window_s;/* <= 480 */
+  int32_t _pad;
+  ccka_hpa_policy policies[2];
+} ccka_hpa_rules;
+
+typedef struct ccka_deployment {
+  int32_t scaler;           /* CCKA_SCALER_* */
+  int32_t replicas0;
+  int32_t min_replicas;
+  int32_t max_replicas;
+  int32_t target_util_pct;  /* HPA averageUtilization */
+  int32_t req_cpu_m;
+  int32_t req_mem_mi;
+  int32_t limit_cpu_m;
+  uint32_t cap_sel;         /* nodeSelector capacity-type bits, 3 = none */
+  int32_t pdb_member;       /* selected by the PDB */
+  int32_t keda_cooldown_s;
+  int32_t keda_min;
+  int32_t keda_max;
+  int32_t _pad;
+  int64_t keda_threshold;   /* AverageValue target per replica (metric units) */
+  int64_t keda_activation;  /* activationThreshold */
+  double tolerance;         /* 0.1 */
+  ccka_hpa_rules up;
+  ccka_hpa_rules down;
+} ccka_deployment;
+
+/* Everything batch-uniform. Array pointers are HOST pointers. */
+typedef struct ccka_world {
+  int32_t n_steps;
+  int32_t start_minute;
+  int32_t provision_delay_steps;
+  int32_t max_nodes;            /* Karpenter node slots per scenario (<= 16) */
+
+  int32_t n_types;
+  int32_t n_regions;
+  int32_t n_zones;
+  int32_t n_pools;
+  const ccka_itype* types;      /* [n_types]                         */
+  const double* ci_gpwh;        /* [n_regions][24]                   */
+  const double* ci_gpwmin;      /* [n_regions][24]                   */
+  const int32_t* price_uph;     /* [n_regions][24][n_types][n_zones][2] */
+
+  ccka_pool pools[CCKA_MAX_POOLS];
+  int32_t n_deploy;
+  int32_t base_nodes;
+  int32_t base_type;
+  int32_t slo_util_pct;
+  ccka_deployment deploy[CCKA_MAX_DEPLOY];
+
+  double base_util;
+  double carbon_weight;         /* $/kgCO2 (default; per-scenario override) */
+  int32_t pdb_min_available_pct;/* -1 none */
+  int32_t peak_start_min;
+  int32_t peak_end_min;
+  int32_t peak_switch;          /* 1: peak/off-peak switch on            */
+  int32_t reset_ca_s;           /* consolidateAfter of the RESET profile */
+  int32_t _pad;
+} ccka_world;
+
+/* Per-scenario parameters, SoA, host pointers. NULL ⇒ world default. */
+typedef struct ccka_scenarios {
+  int64_t n;
+  int64_t first_id;             /* global id of element 0 (trace RNG key) */
+  const uint8_t* region;
+  const int16_t* target_util_pct;
+  const int16_t* max_replicas;
+  const int16_t* down_stab_s;
+  const int16_t* reset_ca_s;
+  const uint8_t* peak_switch;
+  const double* carbon_weight;
+  const uint8_t* cap_sel;       /* nodeSelector override for every deployment */
+} ccka_scenarios;
+
+/* Per-scenario results, SoA, caller-owned host arrays (NULL ⇒ skipped). */
+typedef struct ccka_results {
+  int64_t* cost_uphmin;         /* µ$/h·min; dollars = v/6e7 */
+  double* energy_wmin;          /* W·min; kWh = v/6e4        */
+  double* gco2;
+  int32_t* slo_minutes;
+  int64_t* pending_pod_minutes;
+  int32_t* node_min_spot;
+  int32_t* node_min_od;
+  int32_t* launches;
+  int32_t* deletions;
+  int32_t* peak_nodes;
+  int32_t* final_replicas;
+  int32_t* final_nodes;
+  uint32_t* last_choice;
+  uint32_t* choice_hash;
+} ccka_results;
+
+/* Trajectory record, one per (step, scenario), layout [T][N]. 16 bytes. */
+typedef struct ccka_traj_rec {
+  int32_t replicas;
+  int32_t pending;
+  uint16_t nodes_spot;
+  uint16_t nodes_od;
+  uint16_t last_type;
+  uint16_t flags;
+} ccka_traj_rec;
+
+/* Whole-batch totals (packed for one all-reduce). Integer fields are exact and
+ * order-independent; doubles are summed in a fixed tree order per device. */
+typedef struct ccka_totals {
+  int64_t scenarios;
+  int64_t cost_uphmin;
+  int64_t slo_minutes;
+  int64_t pending_pod_minutes;
+  int64_t node_min_spot;
+  int64_t node_min_od;
+  int64_t launches;
+  int64_t deletions;
+  double energy_wmin;
+  double gco2;
+} ccka_totals;
+
+/* Synthetic load-trace generator (docs/SEMANTICS.md §4). */
+typedef struct ccka_trace_gen {
+  uint64_t seed;
+  int32_t base_lo, base_hi;       /* millicores */
+  int32_t amp_lo_pm, amp_hi_pm;   /* diurnal amplitude, permille */
+  int32_t noise_pm;               /* noise sigma, permille */
+  int32_t burst_prob_pm;
+  int32_t burst_mult_pm;
+  int32_t burst_len;              /* steps */
+} ccka_trace_gen;
+
+typedef struct ccka_ctx ccka_ctx;
+
+/* ---- lifetime -------------------------------------------------------- */
+int32_t ccka_abi_version(void);
+/* sizes of the ABI structs, for binding self-checks: fills out[0..n) in the
+ * order itype, pool, deployment, world, scenarios, results, traj_rec, totals,
+ * trace_gen; returns the count written. */
+int32_t ccka_struct_sizes(int64_t* out, int32_t n);
+int ccka_open(ccka_ctx** out, int device_ordinal);
+void ccka_close(ccka_ctx* ctx);
+const char* ccka_last_error(const ccka_ctx* ctx);
+
+/* ---- inputs ---------------------------------------------------------- */
+/* Validate and upload the world (catalog, tiles, pools, deployments). */
+int ccka_set_world(ccka_ctx* ctx, const ccka_world* world);
+/* Upload per-scenario parameters (resets any previous batch). */
+int ccka_set_scenarios(ccka_ctx* ctx, const ccka_scenarios* sc);
+/* Upload host load traces, layout [T][D][N] int32. */
+int ccka_set_load(ccka_ctx* ctx, const int32_t* load, int64_t count);
+/* Generate load traces on the device (same values as the host generator). */
+int ccka_gen_load(ccka_ctx* ctx, const ccka_trace_gen* gen);
+/* Copy the device-resident traces back ([T][D][N]). */
+int ccka_get_load(ccka_ctx* ctx, int32_t* load, int64_t count);
+
+/* ---- rollout --------------------------------------------------------- */
+/* Run the whole horizon for every scenario. trajectory != 0 also writes
+ * the [T][N] trajectory records on the device. Results stay on the device
+ * until ccka_get_results / ccka_get_trajectory / ccka_get_totals. */
+int ccka_rollout(ccka_ctx* ctx, int32_t trajectory);
+int ccka_rollout_async(ccka_ctx* ctx, int32_t trajectory);
+int ccka_sync(ccka_ctx* ctx);
+/* Duration of the last rollout kernel(s), from HIP events on the engine's
+ * stream (milliseconds). */
+int ccka_last_kernel_ms(ccka_ctx* ctx, double* ms);
+int ccka_get_results(ccka_ctx* ctx, ccka_results* out);
+int ccka_get_trajectory(ccka_ctx* ctx, ccka_traj_rec* out, int64_t count);
+int ccka_get_totals(ccka_ctx* ctx, ccka_totals* out);
+
+/* ---- multi-GPU (RCCL over xGMI) -------------------------------------- */
+/* Fill a 128-byte RCCL unique id (rank 0 only; distribute it out of band). */
+int ccka_comm_unique_id(uint8_t* id128);
+int ccka_comm_init(ccka_ctx* ctx, const uint8_t* id128, int32_t nranks, int32_t rank);
+/* In-place sum of the packed totals across ranks. */
+int ccka_allreduce_totals(ccka_ctx* ctx, ccka_totals* inout);
+
+/* ---- introspection ---------------------------------------------------- */
+/* Name and compute-unit count of the context's device. */
+int ccka_device_info(ccka_ctx* ctx, char* name, int32_t name_len, int32_t* cu_count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCKA_H */

@@ -1,0 +1,829 @@
+/*
+ * ccka_oracle.c — TEST INFRASTRUCTURE: CPU restatement of docs/SEMANTICS.md.
+ *
+ * This file is the checker for the HIP engine and the timed CPU baseline
+ * ("kind": "port" in bench.py). It is deliberately written as plain,
+ * array-based C that follows the spec line by line; it shares no code with
+ * the engine (only the POD declarations of include/ccka.h).
+ *
+ * Reference anchors (the reference is bash + manifests; the arithmetic is the
+ * upstream controllers it drives, see SEMANTICS.md "Parity status"):
+ *   profiles      demo_19_reset_policies.sh:68-75, demo_20_offpeak_configure.sh:59-81,
+ *                 demo_21_peak_configure.sh:56-77 (captured run lines 188-209)
+ *   pods          demo_30_burst_configure.sh:57-141 (nodeSelector :104-105,
+ *                 requests/limits :134-140), PDB demo_10_setup_configure.sh:47-56
+ *   base nodes    01_cluster.sh:24-30, .env:5-8
+ *   HPA           upstream k8s 1.34 (.env:4) horizontal.go / replica_calculator.go
+ *   Karpenter     upstream 1.8.1 (05_karpenter.sh:20) provisioner + disruption
+ *   KEDA          never installed (.env:10-12), ScaledObject semantics
+ *
+ * Build: gcc -O3 -march=native -ffp-contract=off -fPIC -shared -pthread
+ * (see oracle/Makefile). No contraction, no fast-math: every double operation
+ * below is one IEEE binary64 operation in the order SEMANTICS.md states.
+ */
+#include "ccka_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define O_BIG 0x3fffffffffffffffLL
+
+/* ------------------------------------------------------------------------ */
+/* Philox-4x32-10                                                            */
+/* ------------------------------------------------------------------------ */
+void ccka_oracle_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                        uint32_t k0, uint32_t k1, uint32_t* out4) {
+  uint32_t c[4] = {c0, c1, c2, c3};
+  uint32_t k[2] = {k0, k1};
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k[0];
+    uint32_t n1 = lo1;
+    uint32_t n2 = hi0 ^ c[3] ^ k[1];
+    uint32_t n3 = lo0;
+    c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+    k[0] += 0x9E3779B9u;
+    k[1] += 0xBB67AE85u;
+  }
+  out4[0] = c[0]; out4[1] = c[1]; out4[2] = c[2]; out4[3] = c[3];
+}
+
+void ccka_oracle_sin_table(int32_t* out) {
+  for (int m = 0; m < 1440; ++m)
+    out[m] = (int32_t)lround(65536.0 * sin(2.0 * M_PI * (double)m / 1440.0));
+}
+
+void ccka_oracle_gen_load(const ccka_trace_gen* g, int32_t T, int32_t D, int64_t n,
+                          int64_t first_id, int32_t* out) {
+  int32_t sinq[1440];
+  ccka_oracle_sin_table(sinq);
+  const uint32_t k0 = (uint32_t)g->seed, k1 = (uint32_t)(g->seed >> 32);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t s = (uint64_t)(first_id + i);
+    const uint32_t slo = (uint32_t)s, shi = (uint32_t)(s >> 32);
+    for (int32_t d = 0; d < D; ++d) {
+      uint32_t u[4], v[4];
+      ccka_oracle_philox(0xFFFFFFFFu, slo, shi, (uint32_t)d, k0, k1, u);
+      ccka_oracle_philox(0xFFFFFFFEu, slo, shi, (uint32_t)d, k0, k1, v);
+      const int64_t base = g->base_lo + (int64_t)(u[0] % (uint32_t)(g->base_hi - g->base_lo + 1));
+      const int64_t amp = g->amp_lo_pm + (int64_t)(u[1] % (uint32_t)(g->amp_hi_pm - g->amp_lo_pm + 1));
+      const int32_t phase = (int32_t)(u[2] % 1440u);
+      const int burst = (int32_t)(u[3] % 1000u) < g->burst_prob_pm;
+      const int32_t bstart = (int32_t)(v[0] % 1440u);
+      for (int32_t t = 0; t < T; ++t) {
+        uint32_t e4[4];
+        ccka_oracle_philox((uint32_t)t, slo, shi, (uint32_t)d, k0, k1, e4);
+        const int64_t e = (int64_t)(e4[0] >> 16) + (int64_t)(e4[1] >> 16) +
+                          (int64_t)(e4[2] >> 16) + (int64_t)(e4[3] >> 16) - 131072;
+        int64_t val = base * (65536000LL + amp * (int64_t)sinq[(t + phase) % 1440]) / 65536000LL;
+        val = val * (37837000LL + (int64_t)g->noise_pm * e) / 37837000LL;
+        if (burst && t >= bstart && t < bstart + g->burst_len) val = val * g->burst_mult_pm / 1000;
+        if (val < 0) val = 0;
+        if (val > 0x7fffffff) val = 0x7fffffff;
+        out[((int64_t)t * D + d) * n + i] = (int32_t)val;
+      }
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* HPA pieces                                                                */
+/* ------------------------------------------------------------------------ */
+static int o_within(double x, double tol) { return (1.0 - tol) <= x && x <= (1.0 + tol); }
+
+int32_t ccka_oracle_hpa_resource_proposal(int32_t cur, int32_t ready, int64_t usage_m,
+                                          int32_t req_m, int32_t target_pct, double tol,
+                                          int32_t* util_out) {
+  if (ready <= 0 || req_m <= 0) {
+    if (util_out) *util_out = -1;
+    return cur;
+  }
+  const int32_t util = (int32_t)((usage_m * 100) / ((int64_t)ready * req_m));
+  if (util_out) *util_out = util;
+  const double ratio = (double)util / (double)target_pct;
+  const int32_t unready = cur - ready;
+  if (unready > 0 && ratio > 1.0) {
+    /* upstream: unready pods count as 0 usage when scaling up */
+    const int32_t nutil = (int32_t)((usage_m * 100) / ((int64_t)cur * req_m));
+    const double nr = (double)nutil / (double)target_pct;
+    if (o_within(nr, tol) || nr < 1.0) return cur;
+    int32_t p = (int32_t)ceil(nr * (double)cur);
+    if (p < cur) p = cur;
+    return p;
+  }
+  if (o_within(ratio, tol)) return cur;
+  return (int32_t)ceil(ratio * (double)ready);
+}
+
+int32_t ccka_oracle_keda_proposal(int32_t cur, int64_t metric, int64_t threshold, double tol) {
+  const double r = (double)metric / ((double)threshold * (double)cur);
+  if (o_within(r, tol)) return cur;
+  return (int32_t)ceil((double)metric / (double)threshold);
+}
+
+static int32_t o_rate_up(int32_t cur, const ccka_hpa_rules* up, const int32_t* deltas) {
+  if (up->select == CCKA_SELECT_DISABLED) return cur;
+  int64_t res = up->select == CCKA_SELECT_MIN ? INT32_MAX : INT32_MIN;
+  for (int i = 0; i < up->n_policies; ++i) {
+    const ccka_hpa_policy* p = &up->policies[i];
+    int64_t added = 0, deleted = 0;
+    for (int k = 0; k < CCKA_HIST; ++k) {
+      if ((k + 1) * CCKA_STEP_SECONDS < p->period_s) {
+        if (deltas[k] > 0) added += deltas[k];
+        if (deltas[k] < 0) deleted += -deltas[k];
+      }
+    }
+    const int64_t ps = cur - added + deleted;
+    int64_t prop;
+    if (p->type == CCKA_HPA_PODS) prop = ps + p->value;
+    else prop = (int32_t)ceil((double)ps * (1.0 + (double)p->value / 100.0));
+    if (up->select == CCKA_SELECT_MIN) { if (prop < res) res = prop; }
+    else { if (prop > res) res = prop; }
+  }
+  return (int32_t)res;
+}
+
+static int32_t o_rate_down(int32_t cur, const ccka_hpa_rules* dn, const int32_t* deltas) {
+  if (dn->select == CCKA_SELECT_DISABLED) return cur;
+  /* Max selects the policy allowing the biggest change: the minimum count */
+  int64_t res = dn->select == CCKA_SELECT_MIN ? INT32_MIN : INT32_MAX;
+  for (int i = 0; i < dn->n_policies; ++i) {
+    const ccka_hpa_policy* p = &dn->policies[i];
+    int64_t added = 0, deleted = 0;
+    for (int k = 0; k < CCKA_HIST; ++k) {
+      if ((k + 1) * CCKA_STEP_SECONDS < p->period_s) {
+        if (deltas[k] > 0) added += deltas[k];
+        if (deltas[k] < 0) deleted += -deltas[k];
+      }
+    }
+    const int64_t ps = cur - added + deleted;
+    int64_t prop;
+    if (p->type == CCKA_HPA_PODS) prop = ps - p->value;
+    else prop = (int32_t)((double)ps * (1.0 - (double)p->value / 100.0));
+    if (dn->select == CCKA_SELECT_MIN) { if (prop > res) res = prop; }
+    else { if (prop < res) res = prop; }
+  }
+  return (int32_t)res;
+}
+
+int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, int32_t max_r,
+                                 const ccka_hpa_rules* up, const ccka_hpa_rules* down,
+                                 const int32_t* recs, const uint8_t* rec_valid,
+                                 const int32_t* deltas) {
+  /* stabilizeRecommendationWithBehaviors */
+  int32_t upr = proposal, dnr = proposal;
+  for (int k = 0; k < CCKA_HIST; ++k) {
+    if (!rec_valid[k]) continue;
+    const int age = (k + 1) * CCKA_STEP_SECONDS;
+    if (age < up->stab_window_s && recs[k] < upr) upr = recs[k];
+    if (age < down->stab_window_s && recs[k] > dnr) dnr = recs[k];
+  }
+  int32_t rec = cur;
+  if (rec < upr) rec = upr;
+  if (rec > dnr) rec = dnr;
+  /* convertDesiredReplicasWithBehaviorRate */
+  int32_t lo = min_r, hi = max_r;
+  if (rec > cur) {
+    int32_t lim = o_rate_up(cur, up, deltas);
+    if (lim < cur) lim = cur;
+    if (hi > lim) hi = lim;
+  } else if (rec < cur) {
+    int32_t lim = o_rate_down(cur, down, deltas);
+    if (lim > cur) lim = cur;
+    if (lo < lim) lo = lim;
+  }
+  if (rec < lo) return lo;
+  if (rec > hi) return hi;
+  return rec;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Scenario state                                                            */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int used, pool, type, zone, cap, ready_step, last_event;
+  int pods[CCKA_MAX_DEPLOY];
+} o_node;
+
+typedef struct {
+  int policy, ca_s;
+  uint32_t zone_mask, cap_mask;
+} o_pool;
+
+typedef struct {
+  int replicas;
+  int32_t rec[CCKA_HIST];
+  uint8_t rec_valid[CCKA_HIST];
+  int32_t delta[CCKA_HIST];
+  int last_active;
+} o_dep;
+
+typedef struct {
+  int pool, slot;
+  uint32_t cap, zone;
+  int64_t s_cpu, s_mem, s_pods;
+  int pods[CCKA_MAX_DEPLOY];
+} o_claim;
+
+static void o_patch(o_pool* p, const ccka_pool_patch* pp) {
+  if (pp->policy != CCKA_POLICY_KEEP) p->policy = pp->policy;
+  if (pp->consolidate_after_s >= 0) p->ca_s = pp->consolidate_after_s;
+  if (pp->zone_mask) p->zone_mask = pp->zone_mask;
+  if (pp->cap_mask) p->cap_mask = pp->cap_mask;
+}
+
+static int64_t o_usage(int64_t L, int64_t ready, int32_t limit) {
+  if (limit <= 0) return L;
+  const int64_t cap = ready * limit;
+  return L < cap ? L : cap;
+}
+
+/* max additional pods of (rc, rm) on capacity (ac, am, ap) holding (uc, um, up);
+ * -1 when the capacity cannot hold what it already has. */
+static int64_t o_fit(int64_t ac, int64_t am, int64_t ap, int64_t uc, int64_t um, int64_t up,
+                     int32_t rc, int32_t rm) {
+  if (uc > ac || um > am || up > ap) return -1;
+  int64_t f = ap - up;
+  if (rc > 0) { int64_t c = (ac - uc) / rc; if (c < f) f = c; }
+  if (rm > 0) { int64_t m = (am - um) / rm; if (m < f) f = m; }
+  return f;
+}
+
+static int o_capidx_bit(int c) { return c == 0 ? CCKA_CAP_SPOT : CCKA_CAP_OD; }
+
+typedef struct {
+  const ccka_world* w;
+  int T, D, K, Z, N;     /* N = maxnodes */
+  int prov[CCKA_MAX_DEPLOY];
+} o_env;
+
+static int32_t o_price(const o_env* e, int r, int h, int k, int z, int c) {
+  return e->w->price_uph[((((int64_t)r * 24 + h) * e->K + k) * e->Z + z) * 2 + c];
+}
+
+/* node usage of a slot */
+static void o_node_use(const o_env* e, const o_node* nd, int64_t* uc, int64_t* um, int64_t* up) {
+  int64_t c = 0, m = 0, p = 0;
+  for (int d = 0; d < e->D; ++d) {
+    c += (int64_t)nd->pods[d] * e->w->deploy[d].req_cpu_m;
+    m += (int64_t)nd->pods[d] * e->w->deploy[d].req_mem_mi;
+    p += nd->pods[d];
+  }
+  *uc = c; *um = m; *up = p;
+}
+
+static int64_t o_node_fit(const o_env* e, const o_node* nd, int d) {
+  const ccka_itype* ty = &e->w->types[nd->type];
+  int64_t uc, um, up;
+  o_node_use(e, nd, &uc, &um, &up);
+  int64_t f = o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, uc, um, up,
+                    e->w->deploy[d].req_cpu_m, e->w->deploy[d].req_mem_mi);
+  return f < 0 ? 0 : f;
+}
+
+/* type candidate for a claim: holds sums, limit, offered in masks */
+static int o_type_ok(const o_env* e, int r, int h, int k, uint32_t zm, uint32_t cm,
+                     int64_t pool_use, int32_t limit) {
+  const ccka_itype* ty = &e->w->types[k];
+  if (limit >= 0 && pool_use + (int64_t)ty->vcpu * 1000 > limit) return 0;
+  for (int z = 0; z < e->Z; ++z) {
+    if (!(zm >> z & 1u)) continue;
+    for (int c = 0; c < 2; ++c)
+      if ((cm & (uint32_t)o_capidx_bit(c)) && o_price(e, r, h, k, z, c) > 0) return 1;
+  }
+  return 0;
+}
+
+static int64_t o_claim_j(const o_env* e, int r, int h, const o_claim* cl, uint32_t cm, int d,
+                         int64_t pool_use, int32_t limit) {
+  int64_t best = 0;
+  for (int k = 0; k < e->K; ++k) {
+    if (!o_type_ok(e, r, h, k, cl->zone, cm, pool_use, limit)) continue;
+    const ccka_itype* ty = &e->w->types[k];
+    const int64_t f = o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, cl->s_cpu, cl->s_mem,
+                            cl->s_pods, e->w->deploy[d].req_cpu_m, e->w->deploy[d].req_mem_mi);
+    if (f > best) best = f;
+  }
+  return best;
+}
+
+typedef struct {
+  o_pool pools[CCKA_MAX_POOLS];
+  o_dep dep[CCKA_MAX_DEPLOY];
+  o_node nodes[CCKA_MAX_NODES];
+  int profile;
+  int64_t cost, pend_min;
+  double energy, gco2;
+  int slo, nmin_spot, nmin_od, launches, deletions, peak_nodes;
+  uint32_t last_choice, hash;
+} o_state;
+
+static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* load, int64_t i,
+                      int64_t nsc, ccka_results* out, ccka_traj_rec* traj) {
+  const ccka_world* w = e->w;
+  const int D = e->D, NN = e->N, K = e->K;
+  o_state st;
+  memset(&st, 0, sizeof st);
+  const int r = sc->region ? sc->region[i] : 0;
+  const int reset_ca = sc->reset_ca_s ? sc->reset_ca_s[i] : w->reset_ca_s;
+  const int pswitch = sc->peak_switch ? sc->peak_switch[i] : w->peak_switch;
+  const double cw = sc->carbon_weight ? sc->carbon_weight[i] : w->carbon_weight;
+  const double wc1000 = cw * 1000.0;
+  int target[CCKA_MAX_DEPLOY], maxr[CCKA_MAX_DEPLOY];
+  uint32_t capsel[CCKA_MAX_DEPLOY];
+  ccka_hpa_rules downr[CCKA_MAX_DEPLOY];
+  for (int d = 0; d < D; ++d) {
+    const ccka_deployment* dp = &w->deploy[d];
+    target[d] = dp->target_util_pct;
+    maxr[d] = dp->max_replicas;
+    downr[d] = dp->down;
+    capsel[d] = sc->cap_sel ? sc->cap_sel[i] : dp->cap_sel;
+    if (dp->scaler == CCKA_SCALER_HPA) {
+      if (sc->target_util_pct) target[d] = sc->target_util_pct[i];
+      if (sc->max_replicas) maxr[d] = sc->max_replicas[i];
+      if (sc->down_stab_s) downr[d].stab_window_s = sc->down_stab_s[i];
+    }
+    st.dep[d].replicas = dp->replicas0;
+    st.dep[d].last_active = 0;
+  }
+  for (int p = 0; p < w->n_pools; ++p) {
+    memset(&st.pools[p], 0, sizeof(o_pool));
+    o_patch(&st.pools[p], &w->pools[p].base);
+    ccka_pool_patch rp = w->pools[p].profile[CCKA_PROFILE_RESET];
+    if (rp.consolidate_after_s >= 0) rp.consolidate_after_s = reset_ca;
+    o_patch(&st.pools[p], &rp);
+  }
+  st.profile = -1;
+  st.hash = 2166136261u;
+  st.last_choice = 0xFFFFFFFFu;
+  const ccka_itype* bt = &w->types[w->base_type];
+  const double base_w = (double)w->base_nodes * (bt->p_idle_w + bt->p_dyn_w * w->base_util);
+  const int ps = w->peak_start_min, pe = w->peak_end_min;
+
+  for (int t = 0; t < w->n_steps; ++t) {
+    const int minute = (w->start_minute + t) % 1440;
+    const int h = minute / 60;
+    uint16_t flags = 0;
+    uint16_t step_last_type = 0xFFFF;
+    /* ---- A. profile ---- */
+    int in_win = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
+    const int peak = pswitch && in_win;
+    const int prof = peak ? CCKA_PROFILE_PEAK : CCKA_PROFILE_OFFPEAK;
+    if (peak) flags |= 1;
+    if (prof != st.profile) {
+      for (int p = 0; p < w->n_pools; ++p) o_patch(&st.pools[p], &w->pools[p].profile[prof]);
+      st.profile = prof;
+    }
+    /* ---- C. scalers ---- */
+    int util_valid[CCKA_MAX_DEPLOY], util[CCKA_MAX_DEPLOY];
+    int64_t Lt[CCKA_MAX_DEPLOY];
+    for (int d = 0; d < D; ++d) {
+      const ccka_deployment* dp = &w->deploy[d];
+      o_dep* ds = &st.dep[d];
+      const int64_t L = load[((int64_t)t * D + d) * nsc + i];
+      Lt[d] = L;
+      util_valid[d] = 0;
+      util[d] = 0;
+      int ready = 0;
+      for (int n = 0; n < NN; ++n)
+        if (st.nodes[n].used && st.nodes[n].ready_step <= t) ready += st.nodes[n].pods[d];
+      const int cur = ds->replicas;
+      int desired = cur;
+      int ran = 0;           /* HPA normal path ran: store rec */
+      int32_t proposal = cur;
+      int hpa_path = 0;      /* desired produced by the HPA (records delta) */
+      int minr = dp->min_replicas, mx = maxr[d];
+      if (dp->scaler == CCKA_SCALER_HPA) {
+        hpa_path = 1;
+        if (cur == 0 && minr != 0) { desired = 0; hpa_path = 0; }
+        else if (cur > mx) desired = mx;
+        else if (cur < minr) desired = minr;
+        else if (ready == 0) { desired = cur; }
+        else {
+          int32_t u = 0;
+          const int64_t usage = o_usage(L, ready, dp->limit_cpu_m);
+          proposal = ccka_oracle_hpa_resource_proposal(cur, ready, usage, dp->req_cpu_m, target[d],
+                                                       dp->tolerance, &u);
+          util_valid[d] = 1;
+          util[d] = u;
+          desired = ccka_oracle_hpa_behavior(cur, proposal, minr, mx, &dp->up, &downr[d], ds->rec,
+                                             ds->rec_valid, ds->delta);
+          ran = 1;
+        }
+      } else if (dp->scaler == CCKA_SCALER_KEDA) {
+        const int active = L > dp->keda_activation;
+        if (active) ds->last_active = t;
+        if (cur == 0) desired = active ? 1 : 0;
+        else if (!active && dp->keda_min == 0 &&
+                 (int64_t)(t - ds->last_active) * CCKA_STEP_SECONDS >= dp->keda_cooldown_s)
+          desired = 0;
+        else {
+          hpa_path = 1;
+          minr = dp->keda_min > 1 ? dp->keda_min : 1;
+          mx = dp->keda_max;
+          if (cur > mx) desired = mx;
+          else if (cur < minr) desired = minr;
+          else {
+            proposal = ccka_oracle_keda_proposal(cur, L, dp->keda_threshold, dp->tolerance);
+            desired = ccka_oracle_hpa_behavior(cur, proposal, minr, mx, &dp->up, &dp->down, ds->rec,
+                                               ds->rec_valid, ds->delta);
+            ran = 1;
+          }
+        }
+      }
+      if (dp->scaler != CCKA_SCALER_STATIC) {
+        /* shift history rings: entry 0 becomes this step */
+        for (int k = CCKA_HIST - 1; k > 0; --k) {
+          ds->rec[k] = ds->rec[k - 1];
+          ds->rec_valid[k] = ds->rec_valid[k - 1];
+          ds->delta[k] = ds->delta[k - 1];
+        }
+        ds->rec[0] = ran ? proposal : 0;
+        ds->rec_valid[0] = (uint8_t)ran;
+        ds->delta[0] = (hpa_path && desired != cur) ? desired - cur : 0;
+        ds->replicas = desired;
+      }
+    }
+    /* ---- D. ReplicaSet reconcile ---- */
+    for (int d = 0; d < D; ++d) {
+      int total = 0;
+      for (int n = 0; n < NN; ++n) if (st.nodes[n].used) total += st.nodes[n].pods[d];
+      int excess = total - st.dep[d].replicas;
+      for (int pass = 0; pass < 2 && excess > 0; ++pass) {
+        for (int n = NN - 1; n >= 0 && excess > 0; --n) {
+          o_node* nd = &st.nodes[n];
+          if (!nd->used) continue;
+          const int rdy = nd->ready_step <= t;
+          if ((pass == 0 && rdy) || (pass == 1 && !rdy)) continue;
+          if (nd->pods[d] <= 0) continue;
+          const int k = nd->pods[d] < excess ? nd->pods[d] : excess;
+          nd->pods[d] -= k;
+          excess -= k;
+          nd->last_event = t;
+        }
+      }
+    }
+    /* ---- E. kube-scheduler (ready) and F1. nomination (in-flight) ---- */
+    int pend[CCKA_MAX_DEPLOY];
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int d = 0; d < D; ++d) {
+        int total = 0;
+        for (int n = 0; n < NN; ++n) if (st.nodes[n].used) total += st.nodes[n].pods[d];
+        int p = st.dep[d].replicas - total;
+        for (int n = 0; n < NN && p > 0; ++n) {
+          o_node* nd = &st.nodes[n];
+          if (!nd->used) continue;
+          const int rdy = nd->ready_step <= t;
+          if ((pass == 0 && !rdy) || (pass == 1 && rdy)) continue;
+          if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
+          const int64_t f = o_node_fit(e, nd, d);
+          const int k = (int)(f < p ? f : p);
+          if (k > 0) { nd->pods[d] += k; p -= k; nd->last_event = t; }
+        }
+        pend[d] = p;
+      }
+    }
+    /* ---- F2. provisioning ---- */
+    {
+      int64_t pool_use[CCKA_MAX_POOLS];
+      for (int p = 0; p < w->n_pools; ++p) pool_use[p] = 0;
+      int slot_taken[CCKA_MAX_NODES];
+      for (int n = 0; n < NN; ++n) {
+        slot_taken[n] = st.nodes[n].used;
+        if (st.nodes[n].used) pool_use[st.nodes[n].pool] += (int64_t)w->types[st.nodes[n].type].vcpu * 1000;
+      }
+      o_claim claims[CCKA_MAX_NODES];
+      int ncl = 0;
+      for (int oi = 0; oi < D; ++oi) {
+        const int d = e->prov[oi];
+        int rem = pend[d];
+        if (rem <= 0) continue;
+        const ccka_deployment* dp = &w->deploy[d];
+        for (int c = 0; c < ncl && rem > 0; ++c) {
+          o_claim* cl = &claims[c];
+          const uint32_t cm = cl->cap & capsel[d];
+          if (!cm) continue;
+          const int64_t j = o_claim_j(e, r, h, cl, cm, d, pool_use[cl->pool], w->pools[cl->pool].limit_cpu_m);
+          if (j <= 0) continue;
+          const int k = (int)(j < rem ? j : rem);
+          cl->cap = cm;
+          cl->pods[d] += k;
+          cl->s_cpu += (int64_t)k * dp->req_cpu_m;
+          cl->s_mem += (int64_t)k * dp->req_mem_mi;
+          cl->s_pods += k;
+          rem -= k;
+        }
+        while (rem > 0) {
+          int slot = -1;
+          for (int n = 0; n < NN; ++n) if (!slot_taken[n]) { slot = n; break; }
+          if (slot < 0) break;
+          int chosen = -1;
+          int64_t jj = 0;
+          o_claim nc;
+          memset(&nc, 0, sizeof nc);
+          for (int p = 0; p < w->n_pools; ++p) {
+            const uint32_t cm = st.pools[p].cap_mask & capsel[d];
+            if (!cm) continue;
+            nc.pool = p;
+            nc.cap = cm;
+            nc.zone = st.pools[p].zone_mask;
+            const int64_t j = o_claim_j(e, r, h, &nc, cm, d, pool_use[p], w->pools[p].limit_cpu_m);
+            if (j > 0) { chosen = p; jj = j; break; }
+          }
+          if (chosen < 0) break;
+          const int k = (int)(jj < rem ? jj : rem);
+          nc.pool = chosen;
+          nc.cap = st.pools[chosen].cap_mask & capsel[d];
+          nc.zone = st.pools[chosen].zone_mask;
+          nc.slot = slot;
+          nc.pods[d] = k;
+          nc.s_cpu = (int64_t)k * dp->req_cpu_m;
+          nc.s_mem = (int64_t)k * dp->req_mem_mi;
+          nc.s_pods = k;
+          slot_taken[slot] = 1;
+          claims[ncl++] = nc;
+          rem -= k;
+        }
+      }
+      /* launch in creation order */
+      for (int c = 0; c < ncl; ++c) {
+        o_claim* cl = &claims[c];
+        const int32_t limit = w->pools[cl->pool].limit_cpu_m;
+        int spot_only = 0;
+        if (cl->cap & CCKA_CAP_SPOT) {
+          for (int k = 0; k < K && !spot_only; ++k) {
+            const ccka_itype* ty = &w->types[k];
+            if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, cl->s_cpu, cl->s_mem, cl->s_pods, 0, 0) < 0) continue;
+            if (limit >= 0 && pool_use[cl->pool] + (int64_t)ty->vcpu * 1000 > limit) continue;
+            for (int z = 0; z < e->Z; ++z)
+              if ((cl->zone >> z & 1u) && o_price(e, r, h, k, z, 0) > 0) { spot_only = 1; break; }
+          }
+        }
+        int bk = -1, bz = 0, bc = 0;
+        double bs = 0.0;
+        for (int k = 0; k < K; ++k) {
+          const ccka_itype* ty = &w->types[k];
+          if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, cl->s_cpu, cl->s_mem, cl->s_pods, 0, 0) < 0) continue;
+          if (limit >= 0 && pool_use[cl->pool] + (int64_t)ty->vcpu * 1000 > limit) continue;
+          for (int z = 0; z < e->Z; ++z) {
+            if (!(cl->zone >> z & 1u)) continue;
+            for (int cc = 0; cc < 2; ++cc) {
+              if (!(cl->cap & (uint32_t)o_capidx_bit(cc))) continue;
+              if (spot_only && cc != 0) continue;
+              const int32_t pr = o_price(e, r, h, k, z, cc);
+              if (pr <= 0) continue;
+              const double score = (double)pr + wc1000 * (ty->p_ref_w * w->ci_gpwh[r * 24 + h]);
+              if (bk < 0 || score < bs) { bk = k; bz = z; bc = cc; bs = score; }
+            }
+          }
+        }
+        if (bk < 0) { continue; /* dropped: slot stays free */ }
+        o_node* nd = &st.nodes[cl->slot];
+        memset(nd, 0, sizeof *nd);
+        nd->used = 1;
+        nd->pool = cl->pool;
+        nd->type = bk;
+        nd->zone = bz;
+        nd->cap = bc;
+        nd->ready_step = t + w->provision_delay_steps;
+        nd->last_event = t;
+        for (int d = 0; d < D; ++d) nd->pods[d] = cl->pods[d];
+        pool_use[cl->pool] += (int64_t)w->types[bk].vcpu * 1000;
+        st.launches++;
+        st.last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)cl->pool << 16;
+        st.hash = (st.hash ^ st.last_choice) * 16777619u;
+        step_last_type = (uint16_t)bk;
+        flags |= 2;
+      }
+    }
+    /* ---- G. disruption ---- */
+    {
+      int64_t allowed = O_BIG;
+      if (w->pdb_min_available_pct >= 0) {
+        int64_t rdy = 0, reps = 0;
+        for (int d = 0; d < D; ++d) {
+          if (!w->deploy[d].pdb_member) continue;
+          reps += st.dep[d].replicas;
+          for (int n = 0; n < NN; ++n)
+            if (st.nodes[n].used && st.nodes[n].ready_step <= t) rdy += st.nodes[n].pods[d];
+        }
+        const int64_t desired_healthy = (w->pdb_min_available_pct * reps + 99) / 100;
+        allowed = rdy - desired_healthy;
+        if (allowed < 0) allowed = 0;
+      }
+      for (int p = 0; p < w->n_pools; ++p) {
+        int npool = 0;
+        for (int n = 0; n < NN; ++n) if (st.nodes[n].used && st.nodes[n].pool == p) npool++;
+        if (npool == 0) continue;
+        const int budget = (w->pools[p].budget_pct * npool + 99) / 100;
+        int deleted = 0;
+        int rejected[CCKA_MAX_NODES] = {0};
+        while (deleted < budget) {
+          int best = -1, bpods = 0;
+          int32_t bprice = 0;
+          for (int n = 0; n < NN; ++n) {
+            const o_node* nd = &st.nodes[n];
+            if (!nd->used || nd->pool != p || nd->ready_step > t || rejected[n]) continue;
+            if ((int64_t)(t - nd->last_event) * CCKA_STEP_SECONDS < st.pools[p].ca_s) continue;
+            int pods = 0;
+            for (int d = 0; d < D; ++d) pods += nd->pods[d];
+            if (pods > 0 && st.pools[p].policy != CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) continue;
+            const int32_t pr = o_price(e, r, h, nd->type, nd->zone, nd->cap);
+            if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) {
+              best = n; bpods = pods; bprice = pr;
+            }
+          }
+          if (best < 0) break;
+          int ok = 1;
+          int64_t pdb_pods = 0;
+          o_node trial[CCKA_MAX_NODES];
+          memcpy(trial, st.nodes, sizeof(o_node) * (size_t)NN);
+          if (bpods > 0) {
+            for (int d = 0; d < D; ++d) if (w->deploy[d].pdb_member) pdb_pods += trial[best].pods[d];
+            if (pdb_pods > allowed) ok = 0;
+            for (int d = 0; d < D && ok; ++d) {
+              int need = trial[best].pods[d];
+              for (int n = 0; n < NN && need > 0; ++n) {
+                o_node* nd = &trial[n];
+                if (n == best || !nd->used || nd->ready_step > t) continue;
+                if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
+                const int64_t f = o_node_fit(e, nd, d);
+                const int k = (int)(f < need ? f : need);
+                if (k > 0) { nd->pods[d] += k; need -= k; nd->last_event = t; }
+              }
+              if (need > 0) ok = 0;
+            }
+          }
+          if (!ok) { rejected[best] = 1; continue; }
+          memcpy(st.nodes, trial, sizeof(o_node) * (size_t)NN);
+          memset(&st.nodes[best], 0, sizeof(o_node));
+          allowed -= pdb_pods;
+          deleted++;
+          st.deletions++;
+          flags |= 4;
+        }
+      }
+    }
+    /* ---- H. accounting ---- */
+    {
+      int64_t cost = (int64_t)w->base_nodes * o_price(e, r, h, w->base_type, 0, 1);
+      int ready_d[CCKA_MAX_DEPLOY];
+      double upp[CCKA_MAX_DEPLOY];
+      for (int d = 0; d < D; ++d) {
+        int rd = 0;
+        for (int n = 0; n < NN; ++n)
+          if (st.nodes[n].used && st.nodes[n].ready_step <= t) rd += st.nodes[n].pods[d];
+        ready_d[d] = rd;
+        upp[d] = rd > 0 ? (double)o_usage(Lt[d], rd, w->deploy[d].limit_cpu_m) / (double)rd : 0.0;
+      }
+      double step_w = base_w;
+      int nsp = 0, nod = 0;
+      for (int n = 0; n < NN; ++n) {
+        const o_node* nd = &st.nodes[n];
+        if (!nd->used) continue;
+        const ccka_itype* ty = &w->types[nd->type];
+        cost += o_price(e, r, h, nd->type, nd->zone, nd->cap);
+        double u = 0.0;
+        if (nd->ready_step <= t) {
+          double x = 0.0;
+          for (int d = 0; d < D; ++d) x += (double)nd->pods[d] * upp[d];
+          u = x * ty->inv_alloc_cpu;
+          if (u > 1.0) u = 1.0;
+        }
+        step_w += ty->p_idle_w + ty->p_dyn_w * u;
+        if (nd->cap == 0) nsp++; else nod++;
+      }
+      st.cost += cost;
+      st.energy += step_w;
+      st.gco2 += step_w * w->ci_gpwmin[r * 24 + h];
+      int pending = 0, viol = 0, reps = 0;
+      for (int d = 0; d < D; ++d) {
+        pending += st.dep[d].replicas - ready_d[d];
+        reps += st.dep[d].replicas;
+        const ccka_deployment* dp = &w->deploy[d];
+        if (dp->scaler == CCKA_SCALER_HPA && util_valid[d] && util[d] > w->slo_util_pct) viol = 1;
+        if (dp->scaler == CCKA_SCALER_KEDA && Lt[d] > dp->keda_activation && st.dep[d].replicas == 0) viol = 1;
+      }
+      if (pending > 0) viol = 1;
+      if (viol) { st.slo++; flags |= 8; }
+      st.pend_min += pending;
+      st.nmin_spot += nsp;
+      st.nmin_od += nod;
+      if (nsp + nod > st.peak_nodes) st.peak_nodes = nsp + nod;
+      if (traj) {
+        ccka_traj_rec* tr = &traj[(int64_t)t * nsc + i];
+        tr->replicas = reps;
+        tr->pending = pending;
+        tr->nodes_spot = (uint16_t)nsp;
+        tr->nodes_od = (uint16_t)nod;
+        tr->last_type = step_last_type;
+        tr->flags = flags;
+      }
+    }
+  }
+  int reps = 0, nodes = 0;
+  for (int d = 0; d < D; ++d) reps += st.dep[d].replicas;
+  for (int n = 0; n < NN; ++n) nodes += st.nodes[n].used;
+  if (out->cost_uphmin) out->cost_uphmin[i] = st.cost;
+  if (out->energy_wmin) out->energy_wmin[i] = st.energy;
+  if (out->gco2) out->gco2[i] = st.gco2;
+  if (out->slo_minutes) out->slo_minutes[i] = st.slo;
+  if (out->pending_pod_minutes) out->pending_pod_minutes[i] = st.pend_min;
+  if (out->node_min_spot) out->node_min_spot[i] = st.nmin_spot;
+  if (out->node_min_od) out->node_min_od[i] = st.nmin_od;
+  if (out->launches) out->launches[i] = st.launches;
+  if (out->deletions) out->deletions[i] = st.deletions;
+  if (out->peak_nodes) out->peak_nodes[i] = st.peak_nodes;
+  if (out->final_replicas) out->final_replicas[i] = reps;
+  if (out->final_nodes) out->final_nodes[i] = nodes;
+  if (out->last_choice) out->last_choice[i] = st.last_choice;
+  if (out->choice_hash) out->choice_hash[i] = st.hash;
+}
+
+typedef struct {
+  const o_env* e;
+  const ccka_scenarios* sc;
+  const int32_t* load;
+  ccka_results* out;
+  ccka_traj_rec* traj;
+  int64_t lo, hi;
+} o_job;
+
+static void* o_worker(void* arg) {
+  o_job* j = (o_job*)arg;
+  for (int64_t i = j->lo; i < j->hi; ++i) o_run_one(j->e, j->sc, j->load, i, j->sc->n, j->out, j->traj);
+  return NULL;
+}
+
+int ccka_oracle_rollout(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
+                        ccka_results* out, ccka_traj_rec* traj, int32_t n_threads) {
+  if (!w || !sc || !load || !out || w->n_deploy < 1 || w->n_deploy > CCKA_MAX_DEPLOY ||
+      w->max_nodes < 1 || w->max_nodes > CCKA_MAX_NODES || w->n_types < 1 || w->n_zones < 1 ||
+      w->n_zones > CCKA_MAX_ZONES || w->n_pools < 1 || w->n_pools > CCKA_MAX_POOLS)
+    return CCKA_EINVAL;
+  o_env e;
+  e.w = w;
+  e.T = w->n_steps;
+  e.D = w->n_deploy;
+  e.K = w->n_types;
+  e.Z = w->n_zones;
+  e.N = w->max_nodes;
+  /* provisioning order: req_cpu desc, req_mem desc, index asc (insertion sort, stable) */
+  for (int d = 0; d < e.D; ++d) e.prov[d] = d;
+  for (int a = 1; a < e.D; ++a) {
+    const int x = e.prov[a];
+    int b = a - 1;
+    while (b >= 0) {
+      const ccka_deployment* P = &w->deploy[e.prov[b]];
+      const ccka_deployment* X = &w->deploy[x];
+      const int before = X->req_cpu_m > P->req_cpu_m ||
+                         (X->req_cpu_m == P->req_cpu_m && X->req_mem_mi > P->req_mem_mi);
+      if (!before) break;
+      e.prov[b + 1] = e.prov[b];
+      --b;
+    }
+    e.prov[b + 1] = x;
+  }
+  if (n_threads < 1) n_threads = 1;
+  if ((int64_t)n_threads > sc->n) n_threads = (int32_t)(sc->n > 0 ? sc->n : 1);
+  pthread_t th[256];
+  o_job jobs[256];
+  if (n_threads > 256) n_threads = 256;
+  for (int k = 0; k < n_threads; ++k) {
+    jobs[k].e = &e;
+    jobs[k].sc = sc;
+    jobs[k].load = load;
+    jobs[k].out = out;
+    jobs[k].traj = traj;
+    jobs[k].lo = sc->n * k / n_threads;
+    jobs[k].hi = sc->n * (k + 1) / n_threads;
+  }
+  if (n_threads == 1) {
+    o_worker(&jobs[0]);
+  } else {
+    for (int k = 0; k < n_threads; ++k) pthread_create(&th[k], NULL, o_worker, &jobs[k]);
+    for (int k = 0; k < n_threads; ++k) pthread_join(th[k], NULL);
+  }
+  return CCKA_OK;
+}
+
+void ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* o) {
+  memset(o, 0, sizeof *o);
+  o->scenarios = n;
+  for (int64_t i = 0; i < n; ++i) {
+    o->cost_uphmin += r->cost_uphmin[i];
+    o->slo_minutes += r->slo_minutes[i];
+    o->pending_pod_minutes += r->pending_pod_minutes[i];
+    o->node_min_spot += r->node_min_spot[i];
+    o->node_min_od += r->node_min_od[i];
+    o->launches += r->launches[i];
+    o->deletions += r->deletions[i];
+    o->energy_wmin += r->energy_wmin[i];
+    o->gco2 += r->gco2[i];
+  }
+}
