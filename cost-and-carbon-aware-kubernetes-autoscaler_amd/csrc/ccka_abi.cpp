@@ -396,11 +396,17 @@ static int plan_launch(ccka_ctx* c, int* block, size_t* lds) {
   k.lds_off_cap1 = (int32_t)off;
   off = up16(off + K * 4);
   k.lds_off_tile = (int32_t)off;
-  off = up16(off + (size_t)span * K * w.n_zones * 2 * 4);
+  const size_t tile_bytes = (size_t)span * K * w.n_zones * 2 * 4;
+  // stage all 24 hourly tiles when they fit comfortably (no barrier in the step
+  // loop); otherwise one hour at a time, restaged at each hour boundary
+  k.all_hours = (off + 24 * tile_bytes + 8 * 1024) <= 64 * 1024 ? 1 : 0;
+  off = up16(off + (k.all_hours ? 24 : 1) * tile_bytes);
   k.lds_off_claims = (int32_t)off;
   off = up16(off + (size_t)(B / 64) * nmax * (7 + dmax) * 4);
   k.lds_off_misc = (int32_t)off;
   off += 16;
+  k.lds_off_ci = (int32_t)off;
+  off = up16(off + (size_t)span * 24 * 2 * sizeof(double));
   if (off > 160 * 1024) return fail(c, CCKA_EINVAL, "LDS budget %zu B exceeds 160 KiB (catalog %zu types, span %d)", off, K, span);
   k.span = span;
   *block = B;
@@ -570,6 +576,14 @@ int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
     return fail(c, CCKA_ERCCL, "ncclAllReduce failed");
   HIPCHK(c, hipMemcpyAsync(io, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+// Internal profiling hook (not part of include/ccka.h): phase-ablation mask
+// for timing attribution only; results of an ablated run are meaningless.
+int ccka_debug_ablate(ccka_ctx* c, int32_t mask) {
+  if (!c) return CCKA_EINVAL;
+  c->kp.ablate = mask;
   return CCKA_OK;
 }
 

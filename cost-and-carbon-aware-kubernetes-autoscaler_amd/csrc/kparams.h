@@ -40,8 +40,9 @@ struct KParams {
   uint32_t* hash;
   ccka_traj_rec* traj;  // nullable
   int64_t N;
-  int32_t T, D, K, Z, R, P, maxn, span;
-  int32_t lds_off_cap1, lds_off_tile, lds_off_claims, lds_off_misc;
+  int32_t T, D, K, Z, R, P, maxn, span, all_hours;
+  int32_t lds_off_cap1, lds_off_tile, lds_off_claims, lds_off_misc, lds_off_ci;
+  int32_t ablate;  // profiling-only phase switches (0 in every real run)
   int32_t prov[CCKA_MAX_DEPLOY];
 };
 

@@ -34,8 +34,10 @@
 
 namespace ccka {
 
+#define CONSTANT __attribute__((address_space(4)))
+typedef const CONSTANT ccka_world CWorld;
+
 constexpr int WAVE = 64;
-constexpr int BIGFIT = 0x3fffffff;
 constexpr int CLAIM_FIXED = 7;  // pool, cap, zone, slot, s_cpu, s_mem, s_pods
 
 __device__ __forceinline__ int rdl(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
@@ -129,20 +131,21 @@ __device__ __forceinline__ uint32_t ni_make(int pool, int type, int zone, int ca
 struct Lds {
   ccka_itype* types;   // [K]
   int* cap1;           // [K] pod capacity of deployment 0 from empty (D == 1 path)
-  int* tile;           // [span][K][Z][2]
+  int* tile;           // current hour: region rl at tile + rl * rstride
+  int rstride;         // ints per region: one hour's tile, or all 24 (all_hours)
   int* claims;         // [waves][MAXN][CLAIM_FIXED + DMAX]
   int K, Z, rmin;
 };
 
 __device__ __forceinline__ int tprice(const Lds& L, int rl, int k, int z, int c) {
-  return L.tile[((rl * L.K + k) * L.Z + z) * 2 + c];
+  return L.tile[rl * L.rstride + (k * L.Z + z) * 2 + c];
 }
 
 // largest pod count of deployment d that fits on type k given sums; -1 if the
 // type cannot hold the sums. (SEMANTICS §3.E fit rule)
 template <int DMAX>
-__device__ __forceinline__ int type_fit(const Lds& L, const KParams& p, int k, int s_cpu, int s_mem,
-                                        int s_pods, int d) {
+__device__ __forceinline__ int type_fit(const Lds& L, int k, int s_cpu, int s_mem, int s_pods, int rc,
+                                        int rm) {
   if (DMAX == 1) {
     const int c = L.cap1[k];
     return c >= s_pods ? c - s_pods : -1;  // exact: floor((A - p*r)/r) = floor(A/r) - p
@@ -150,7 +153,6 @@ __device__ __forceinline__ int type_fit(const Lds& L, const KParams& p, int k, i
   const ccka_itype& ty = L.types[k];
   if (s_cpu > ty.alloc_cpu_m || s_mem > ty.alloc_mem_mi || s_pods > ty.max_pods) return -1;
   int f = ty.max_pods - s_pods;
-  const int rc = p.w->deploy[d].req_cpu_m, rm = p.w->deploy[d].req_mem_mi;
   if (rc > 0) f = min(f, (ty.alloc_cpu_m - s_cpu) / rc);
   if (rm > 0) f = min(f, (ty.alloc_mem_mi - s_mem) / rm);
   return f;
@@ -179,12 +181,12 @@ __device__ __forceinline__ bool limit_ok(const Lds& L, int k, int use, int limit
 // wave-cooperative j (max additional pods of d over candidate types). All
 // arguments are wave-uniform.
 template <int DMAX>
-__device__ int wave_claim_j(const Lds& L, const KParams& p, int rl, uint32_t zm, uint32_t cm,
-                            int s_cpu, int s_mem, int s_pods, int d, int use, int limit, int lane) {
+__device__ int wave_claim_j(const Lds& L, int rl, uint32_t zm, uint32_t cm, int s_cpu, int s_mem,
+                            int s_pods, int rc, int rm, int use, int limit, int lane) {
   int best = 0;
   for (int k = lane; k < L.K; k += WAVE) {
     if (!limit_ok(L, k, use, limit)) continue;
-    const int f = type_fit<DMAX>(L, p, k, s_cpu, s_mem, s_pods, d);
+    const int f = type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, rc, rm);
     if (f <= best) continue;
     if (!type_offered(L, rl, k, zm, cm)) continue;
     best = f;
@@ -227,10 +229,108 @@ __device__ int wave_launch(const Lds& L, int rl, uint32_t zm, uint32_t cm, int s
   return bi == 0x7fffffff ? -1 : bi;
 }
 
+// 32-bit fast path of util = int32(usage*100 / (ready*req)) (exact: taken only
+// when both operands fit in 31 bits; the int64 divide is a long software
+// sequence on the GPU)
+__device__ __forceinline__ int util_div(long long usage, long long den) {
+  const long long num = usage * 100;
+  if (num < 0x7fffffffLL && den < 0x7fffffffLL) return (int)((unsigned)num / (unsigned)den);
+  return (int)(num / den);
+}
+
+// HPA behavior rules of one direction, hoisted into registers. wmask bit k:
+// a record k+1 steps old is inside the policy period / stabilisation window.
+struct Rule {
+  int sel, n, stab_mask;
+  int type[2], value[2], pmask[2];
+  double factor[2];  // Percent: 1 +/- value/100 (computed exactly as the spec writes it)
+};
+
+// Hot deployment fields, hoisted out of the step loop into registers. Loaded
+// once through a generic pointer: the compiler must keep them in registers
+// (it cannot re-issue the loads across the loop's stores), so the loop runs
+// with no scalar-memory waits (SMEM and LDS share lgkmcnt).
+struct Dep {
+  int scaler, minr, req_cpu, req_mem, limit, pdb, kmin, kmax, kcool;
+  long long kthr, kact;
+  double lo, hi;
+  Rule up, dn;
+};
+
+__device__ __forceinline__ int window_mask(int window_s) {
+  int m = 0;
+#pragma unroll
+  for (int k = 0; k < CCKA_HIST; ++k) m |= ((k + 1) * CCKA_STEP_SECONDS < window_s) ? (1 << k) : 0;
+  return m;
+}
+
+__device__ __forceinline__ Rule load_rule(const ccka_hpa_rules* r, bool up) {
+  Rule o;
+  o.sel = r->select;
+  o.n = r->n_policies;
+  o.stab_mask = window_mask(r->stab_window_s);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    o.type[q] = r->policies[q].type;
+    o.value[q] = r->policies[q].value;
+    o.pmask[q] = window_mask(r->policies[q].period_s);
+    o.factor[q] = up ? (1.0 + (double)o.value[q] / 100.0) : (1.0 - (double)o.value[q] / 100.0);
+  }
+  return o;
+}
+
+__device__ __forceinline__ Dep load_dep(const ccka_deployment* d) {
+  Dep o;
+  o.scaler = d->scaler;
+  o.minr = d->min_replicas;
+  o.req_cpu = d->req_cpu_m;
+  o.req_mem = d->req_mem_mi;
+  o.limit = d->limit_cpu_m;
+  o.pdb = d->pdb_member;
+  o.kmin = d->keda_min;
+  o.kmax = d->keda_max;
+  o.kcool = d->keda_cooldown_s;
+  o.kthr = d->keda_threshold;
+  o.kact = d->keda_activation;
+  o.lo = 1.0 - d->tolerance;
+  o.hi = 1.0 + d->tolerance;
+  o.up = load_rule(&d->up, true);
+  o.dn = load_rule(&d->down, false);
+  return o;
+}
+
+// rate limit of one direction (convertDesiredReplicasWithBehaviorRate)
+__device__ __forceinline__ int rate_limit(const Rule& R, bool up, int cur, const int* delta) {
+  if (R.sel == CCKA_SELECT_DISABLED) return cur;
+  const bool min_sel = R.sel == CCKA_SELECT_MIN;
+  long long res = (up == min_sel) ? 0x7fffffffLL : -0x80000000LL;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q >= R.n) break;
+    int added = 0, removed = 0;
+#pragma unroll
+    for (int k = 0; k < CCKA_HIST; ++k)
+      if (R.pmask[q] >> k & 1) {
+        added += max(delta[k], 0);
+        removed += max(-delta[k], 0);
+      }
+    const long long pst = (long long)cur - added + removed;
+    long long pr;
+    if (R.type[q] == CCKA_HPA_PODS) pr = up ? pst + R.value[q] : pst - R.value[q];
+    else if (up) pr = (int)ceil((double)pst * R.factor[q]);
+    else pr = (int)((double)pst * R.factor[q]);
+    res = (up == min_sel) ? min(res, pr) : max(res, pr);
+  }
+  return (int)res;
+}
+
 template <int DMAX, int MAXN>
 __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const ccka_world* __restrict__ w = p.w;
+  // world through the constant address space for rare (profile-switch) reads;
+  // hot fields are hoisted into registers below
+  CWorld* w = (CWorld*)p.w;
+  const ccka_world* gw = p.w;
   const int K = p.K, Z = p.Z, D = p.D, NP = p.P, NN = p.maxn;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
@@ -244,6 +344,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   L.tile = reinterpret_cast<int*>(smem + p.lds_off_tile);
   L.claims = reinterpret_cast<int*>(smem + p.lds_off_claims) + wid * MAXN * (CLAIM_FIXED + DMAX);
   int* s_rng = reinterpret_cast<int*>(smem + p.lds_off_misc);
+  double* s_ci = reinterpret_cast<double*>(smem + p.lds_off_ci);  // [span][24][gpwmin, gpwh]
 
   // ---- stage the catalog, the region range of this block ----
   for (int k = tid; k < K; k += blockDim.x) {
@@ -265,48 +366,81 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   L.rmin = s_rng[0] == 0x7fffffff ? 0 : s_rng[0];
   const int rl = active ? my_r - L.rmin : 0;
   const int tile_ints = K * Z * 2;
+  int* const tile_base = L.tile;
+  for (int x = tid; x < p.span * 24; x += blockDim.x) {
+    const int rg = min(L.rmin + x / 24, p.R - 1);
+    s_ci[x * 2 + 0] = p.ci_gpwmin[rg * 24 + x % 24];
+    s_ci[x * 2 + 1] = p.ci_gpwh[rg * 24 + x % 24];
+  }
+  __syncthreads();
+  L.rstride = p.all_hours ? 24 * tile_ints : tile_ints;
+  if (p.all_hours) {
+    // small catalogs: stage every hour's tiles once -> no barrier in the step loop
+    for (int rr = 0; rr < p.span; ++rr) {
+      const int rg = L.rmin + rr;
+      if (rg >= p.R) break;
+      const int* src = p.price + (int64_t)rg * 24 * tile_ints;
+      for (int x = tid; x < 24 * tile_ints; x += blockDim.x) tile_base[rr * 24 * tile_ints + x] = src[x];
+    }
+    __syncthreads();
+  }
+
+  // ---- hoisted world fields ----
+  Dep dep[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) dep[d] = load_dep(&gw->deploy[d < D ? d : 0]);
+  int pbudget[CCKA_MAX_POOLS], plimit[CCKA_MAX_POOLS];
+#pragma unroll
+  for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
+    pbudget[q] = gw->pools[q].budget_pct;
+    plimit[q] = gw->pools[q].limit_cpu_m;
+  }
+  const int pdb_pct = gw->pdb_min_available_pct;
+  const int slo_util = gw->slo_util_pct;
+  const int base_nodes = gw->base_nodes, base_type = gw->base_type;
 
   // ---- per-scenario parameters ----
-  const double cw = active && p.cw ? p.cw[i] : w->carbon_weight;
+  const double cw = active && p.cw ? p.cw[i] : gw->carbon_weight;
   const double wc1000 = cw * 1000.0;
-  const int reset_ca = active && p.reset_ca ? (int)p.reset_ca[i] : w->reset_ca_s;
-  const int pswitch = active && p.pswitch ? (int)p.pswitch[i] : w->peak_switch;
+  const int reset_ca = active && p.reset_ca ? (int)p.reset_ca[i] : gw->reset_ca_s;
+  const int pswitch = active && p.pswitch ? (int)p.pswitch[i] : gw->peak_switch;
 
-  int target[DMAX], maxr[DMAX], dstab[DMAX];
+  int target[DMAX], maxr[DMAX], dnmask[DMAX];
   uint32_t capsel[DMAX];
-  int replicas[DMAX], last_active[DMAX];
+  int replicas[DMAX], last_active[DMAX], placed[DMAX], rpods[DMAX];
   int rec[DMAX][CCKA_HIST], delta[DMAX][CCKA_HIST];
   uint32_t recv[DMAX];
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
-    const ccka_deployment& dp = w->deploy[d < D ? d : 0];
+    const ccka_deployment& dp = gw->deploy[d < D ? d : 0];
     target[d] = dp.target_util_pct;
     maxr[d] = dp.max_replicas;
-    dstab[d] = dp.down.stab_window_s;
+    int dstab = dp.down.stab_window_s;
     if (active && dp.scaler == CCKA_SCALER_HPA) {
       if (p.target) target[d] = p.target[i];
       if (p.maxr) maxr[d] = p.maxr[i];
-      if (p.down_stab) dstab[d] = p.down_stab[i];
+      if (p.down_stab) dstab = p.down_stab[i];
     }
+    dnmask[d] = window_mask(dstab);
     capsel[d] = active && p.cap_sel ? (uint32_t)p.cap_sel[i] : dp.cap_sel;
-    replicas[d] = dp.replicas0;
+    replicas[d] = d < D ? dp.replicas0 : 0;
     last_active[d] = 0;
+    placed[d] = 0;
+    rpods[d] = 0;
     recv[d] = 0;
 #pragma unroll
     for (int k = 0; k < CCKA_HIST; ++k) { rec[d][k] = 0; delta[d][k] = 0; }
   }
-  // pools: policy | ca_s, zone, cap
-  int ppol[CCKA_MAX_POOLS], pca[CCKA_MAX_POOLS];
+  // pools: current policy, consolidateAfter, zone and capacity-type masks
+  int ppol[CCKA_MAX_POOLS], pca[CCKA_MAX_POOLS], puse[CCKA_MAX_POOLS];
   uint32_t pzm[CCKA_MAX_POOLS], pcm[CCKA_MAX_POOLS];
 #pragma unroll
   for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
-    ppol[q] = 0; pca[q] = 0; pzm[q] = 0; pcm[q] = 0;
+    ppol[q] = 0; pca[q] = 0; pzm[q] = 0; pcm[q] = 0; puse[q] = 0;
     if (q < NP) {
-      const ccka_pool& pl = w->pools[q];
-      const ccka_pool_patch* pp[2] = {&pl.base, &pl.profile[CCKA_PROFILE_RESET]};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const ccka_pool_patch& x = *pp[s];
+        auto& x = s == 0 ? w->pools[q].base : w->pools[q].profile[CCKA_PROFILE_RESET];
         if (x.policy != CCKA_POLICY_KEEP) ppol[q] = x.policy;
         if (x.consolidate_after_s >= 0) pca[q] = s == 1 ? reset_ca : x.consolidate_after_s;
         if (x.zone_mask) pzm[q] = x.zone_mask;
@@ -314,56 +448,110 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       }
     }
   }
+  // node slots; `used` / `rdy` are bitmasks over slots. nprice caches the
+  // slot's offering price for the current hour, ncap (D == 1) its pod capacity.
   uint32_t ninfo[MAXN];
-  int nready[MAXN], nlast[MAXN];
+  int nready[MAXN], nlast[MAXN], nprice[MAXN], ncap[MAXN];
   int npods[MAXN][DMAX];
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
-    ninfo[n] = 0; nready[n] = 0; nlast[n] = 0;
+    ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
   }
+  uint32_t used = 0, rdy = 0;
+  const uint32_t slot_mask = NN >= 32 ? 0xFFFFFFFFu : ((1u << NN) - 1u);
+  int next_ready = 0x7fffffff;  // earliest ready_step among not-ready nodes
+  int nsp = 0, nod = 0;         // Karpenter nodes by capacity type
+  // exact skip of the disruption phase: re-evaluate only when something it
+  // depends on changed (g_dirty) or a node crosses its consolidateAfter /
+  // readiness threshold (g_wake)
+  bool g_dirty = true;
+  int g_wake = 0;
+
   int profile = -1;
   long long cost = 0, pend_min = 0, burn = 0, base_price = 0;
   double energy = 0.0, gco2 = 0.0, ci_gpwmin = 0.0, ci_gpwh = 0.0;
   int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
   uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
-  const ccka_itype bt = p.types[w->base_type];
-  const double base_w = (double)w->base_nodes * (bt.p_idle_w + bt.p_dyn_w * w->base_util);
-  const int ps = w->peak_start_min, pe = w->peak_end_min;
+  const ccka_itype bt = p.types[base_type];
+  const double base_w = (double)base_nodes * (bt.p_idle_w + bt.p_dyn_w * gw->base_util);
+  const int ps = gw->peak_start_min, pe = gw->peak_end_min;
+  const int delay = gw->provision_delay_steps;
 
+  // load samples are software-pipelined one step ahead: the HBM latency of
+  // step t+1's coalesced read hides behind step t's decision work
+  int Lnext[DMAX];
+  const int32_t* lptr = p.load + (active ? i : 0);
+  const int64_t lstride = p.N;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) Lnext[d] = lptr[(d < D ? d : 0) * lstride];
+  int minute = gw->start_minute % 1440;
   int hour = -1;
-  for (int t = 0; t < p.T; ++t) {
-    const int minute = (w->start_minute + t) % 1440;
+
+  for (int t = 0; t < p.T; ++t, minute = minute == 1439 ? 0 : minute + 1) {
+    int Lcur[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      Lcur[d] = Lnext[d];
+      // unconditional (clamped) load: lets the compiler count vmcnt exactly
+      // instead of draining every outstanding store at the loop back-edge
+      const int tn = t + 1 < p.T ? t + 1 : t;
+      Lnext[d] = lptr[((int64_t)tn * D + (d < D ? d : 0)) * lstride];
+    }
     const int h = minute / 60;
-    if (h != hour) {  // block-uniform: stage this hour's price tiles
+    if (h != hour) {  // block-uniform: this hour's price tiles
       hour = h;
-      __syncthreads();
-      for (int rr = 0; rr < p.span; ++rr) {
-        const int rg = L.rmin + rr;
-        if (rg >= p.R) break;
-        const int* src = p.price + ((int64_t)rg * 24 + h) * tile_ints;
-        for (int x = tid; x < tile_ints; x += blockDim.x) L.tile[rr * tile_ints + x] = src[x];
+      if (p.all_hours) {
+        L.tile = tile_base + h * tile_ints;
+      } else {
+        __syncthreads();
+        for (int rr = 0; rr < p.span; ++rr) {
+          const int rg = L.rmin + rr;
+          if (rg >= p.R) break;
+          const int* src = p.price + ((int64_t)rg * 24 + h) * tile_ints;
+          for (int x = tid; x < tile_ints; x += blockDim.x) tile_base[rr * tile_ints + x] = src[x];
+        }
+        __syncthreads();
       }
-      __syncthreads();
       if (active) {
-        ci_gpwmin = p.ci_gpwmin[my_r * 24 + h];
-        ci_gpwh = p.ci_gpwh[my_r * 24 + h];
-        base_price = (long long)w->base_nodes * tprice(L, rl, w->base_type, 0, 1);
+        ci_gpwmin = s_ci[(rl * 24 + h) * 2 + 0];
+        ci_gpwh = s_ci[(rl * 24 + h) * 2 + 1];
+        base_price = (long long)base_nodes * tprice(L, rl, base_type, 0, 1);
         burn = 0;
 #pragma unroll
-        for (int n = 0; n < MAXN; ++n)
-          if (ni_used(ninfo[n]))
-            burn += tprice(L, rl, ni_type(ninfo[n]), ni_zone(ninfo[n]), ni_cap(ninfo[n]));
+        for (int n = 0; n < MAXN; ++n) {
+          if (used >> n & 1u) {
+            nprice[n] = tprice(L, rl, ni_type(ninfo[n]), ni_zone(ninfo[n]), ni_cap(ninfo[n]));
+            burn += nprice[n];
+          }
+        }
       }
     }
     uint32_t flags = 0;
     int step_last_type = 0xFFFF;
-    int util_valid[DMAX], util[DMAX], Lt[DMAX], pend[DMAX];
+    int util_valid[DMAX], util[DMAX], pend[DMAX];
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; Lt[d] = 0; pend[d] = 0; }
+    for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; pend[d] = 0; }
 
     if (active) {
+      // ---- B. readiness transitions (nominated pods start running) ----
+      if (t >= next_ready) {
+        next_ready = 0x7fffffff;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) {
+          if ((used & ~rdy) >> n & 1u) {
+            if (nready[n] <= t) {
+              rdy |= 1u << n;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) rpods[d] += npods[n][d];
+            } else {
+              next_ready = min(next_ready, nready[n]);
+            }
+          }
+        }
+        g_dirty = true;
+      }
       // ---- A. profile ----
       const bool in_win = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
       const bool peak = pswitch && in_win;
@@ -371,10 +559,11 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       if (peak) flags |= 1u;
       if (prof != profile) {
         profile = prof;
+        g_dirty = true;
 #pragma unroll
         for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
           if (q >= NP) break;
-          const ccka_pool_patch& x = w->pools[q].profile[prof];
+          auto& x = w->pools[q].profile[prof];
           if (x.policy != CCKA_POLICY_KEEP) ppol[q] = x.policy;
           if (x.consolidate_after_s >= 0) pca[q] = x.consolidate_after_s;
           if (x.zone_mask) pzm[q] = x.zone_mask;
@@ -385,18 +574,14 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d >= D) break;
-        const ccka_deployment& dp = w->deploy[d];
-        const int Lv = p.load[((int64_t)t * D + d) * p.N + i];
-        Lt[d] = Lv;
+        const Dep& dp = dep[d];
+        const int Lv = Lcur[d];
         if (dp.scaler == CCKA_SCALER_STATIC) continue;
-        int ready = 0;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n)
-          if (ni_used(ninfo[n]) && nready[n] <= t) ready += npods[n][d];
+        const int ready = rpods[d];
         const int cur = replicas[d];
         int desired = cur, proposal = cur;
         bool ran = false, hpa_path = false;
-        int minr = dp.min_replicas, mx = maxr[d];
+        int minr = dp.minr, mx = maxr[d];
         bool do_behavior = false;
         if (dp.scaler == CCKA_SCALER_HPA) {
           hpa_path = true;
@@ -405,18 +590,17 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           else if (cur < minr) desired = minr;
           else if (ready > 0) {
             long long usage = Lv;
-            if (dp.limit_cpu_m > 0) usage = min(usage, (long long)ready * dp.limit_cpu_m);
-            const int u = (int)((usage * 100) / ((long long)ready * dp.req_cpu_m));
+            if (dp.limit > 0) usage = min(usage, (long long)ready * dp.limit);
+            const int u = util_div(usage, (long long)ready * dp.req_cpu);
             util_valid[d] = 1;
             util[d] = u;
             const double ratio = (double)u / (double)target[d];
-            const double lo = 1.0 - dp.tolerance, hi = 1.0 + dp.tolerance;
             if (cur - ready > 0 && ratio > 1.0) {
-              const int nu = (int)((usage * 100) / ((long long)cur * dp.req_cpu_m));
+              const int nu = util_div(usage, (long long)cur * dp.req_cpu);
               const double nr = (double)nu / (double)target[d];
-              if ((lo <= nr && nr <= hi) || nr < 1.0) proposal = cur;
+              if ((dp.lo <= nr && nr <= dp.hi) || nr < 1.0) proposal = cur;
               else proposal = max(cur, (int)ceil(nr * (double)cur));
-            } else if (lo <= ratio && ratio <= hi) {
+            } else if (dp.lo <= ratio && ratio <= dp.hi) {
               proposal = cur;
             } else {
               proposal = (int)ceil(ratio * (double)ready);
@@ -424,89 +608,40 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             do_behavior = true;
           }
         } else {  // KEDA
-          const bool act = (long long)Lv > dp.keda_activation;
+          const bool act = (long long)Lv > dp.kact;
           if (act) last_active[d] = t;
           if (cur == 0) desired = act ? 1 : 0;
-          else if (!act && dp.keda_min == 0 && (t - last_active[d]) * CCKA_STEP_SECONDS >= dp.keda_cooldown_s)
+          else if (!act && dp.kmin == 0 && (t - last_active[d]) * CCKA_STEP_SECONDS >= dp.kcool)
             desired = 0;
           else {
             hpa_path = true;
-            minr = max(dp.keda_min, 1);
-            mx = dp.keda_max;
+            minr = max(dp.kmin, 1);
+            mx = dp.kmax;
             if (cur > mx) desired = mx;
             else if (cur < minr) desired = minr;
             else {
-              const double r = (double)Lv / ((double)dp.keda_threshold * (double)cur);
-              const double lo = 1.0 - dp.tolerance, hi = 1.0 + dp.tolerance;
-              proposal = (lo <= r && r <= hi) ? cur : (int)ceil((double)Lv / (double)dp.keda_threshold);
+              const double r = (double)Lv / ((double)dp.kthr * (double)cur);
+              proposal = (dp.lo <= r && r <= dp.hi) ? cur : (int)ceil((double)Lv / (double)dp.kthr);
               do_behavior = true;
             }
           }
         }
-        if (do_behavior) {
+        if (do_behavior && !(p.ablate & 8)) {
           ran = true;
-          // stabilisation
-          const int upw = dp.up.stab_window_s, dnw = dstab[d];
+          // stabilisation over the valid records inside each window
+          const uint32_t upm = recv[d] & (uint32_t)dp.up.stab_mask;
+          const uint32_t dnm = recv[d] & (uint32_t)dnmask[d];
           int upr = proposal, dnr = proposal;
 #pragma unroll
           for (int k = 0; k < CCKA_HIST; ++k) {
-            if (!(recv[d] >> k & 1u)) continue;
-            const int age = (k + 1) * CCKA_STEP_SECONDS;
-            if (age < upw) upr = min(upr, rec[d][k]);
-            if (age < dnw) dnr = max(dnr, rec[d][k]);
+            if (upm >> k & 1u) upr = min(upr, rec[d][k]);
+            if (dnm >> k & 1u) dnr = max(dnr, rec[d][k]);
           }
           int rc = max(cur, upr);
           rc = min(rc, dnr);
           int lo = minr, hi = mx;
-          if (rc > cur) {
-            const ccka_hpa_rules& R = dp.up;
-            int lim = cur;
-            if (R.select != CCKA_SELECT_DISABLED) {
-              long long res = R.select == CCKA_SELECT_MIN ? 0x7fffffffLL : -0x80000000LL;
-              for (int q = 0; q < R.n_policies; ++q) {
-                const ccka_hpa_policy& pol = R.policies[q];
-                int added = 0, removed = 0;
-#pragma unroll
-                for (int k = 0; k < CCKA_HIST; ++k)
-                  if ((k + 1) * CCKA_STEP_SECONDS < pol.period_s) {
-                    added += max(delta[d][k], 0);
-                    removed += max(-delta[d][k], 0);
-                  }
-                const long long pst = (long long)cur - added + removed;
-                long long pr;
-                if (pol.type == CCKA_HPA_PODS) pr = pst + pol.value;
-                else pr = (int)ceil((double)pst * (1.0 + (double)pol.value / 100.0));
-                res = R.select == CCKA_SELECT_MIN ? min(res, pr) : max(res, pr);
-              }
-              lim = (int)res;
-            }
-            lim = max(lim, cur);
-            hi = min(hi, lim);
-          } else if (rc < cur) {
-            const ccka_hpa_rules& R = dp.down;
-            int lim = cur;
-            if (R.select != CCKA_SELECT_DISABLED) {
-              long long res = R.select == CCKA_SELECT_MIN ? -0x80000000LL : 0x7fffffffLL;
-              for (int q = 0; q < R.n_policies; ++q) {
-                const ccka_hpa_policy& pol = R.policies[q];
-                int added = 0, removed = 0;
-#pragma unroll
-                for (int k = 0; k < CCKA_HIST; ++k)
-                  if ((k + 1) * CCKA_STEP_SECONDS < pol.period_s) {
-                    added += max(delta[d][k], 0);
-                    removed += max(-delta[d][k], 0);
-                  }
-                const long long pst = (long long)cur - added + removed;
-                long long pr;
-                if (pol.type == CCKA_HPA_PODS) pr = pst - pol.value;
-                else pr = (int)((double)pst * (1.0 - (double)pol.value / 100.0));
-                res = R.select == CCKA_SELECT_MIN ? max(res, pr) : min(res, pr);
-              }
-              lim = (int)res;
-            }
-            lim = min(lim, cur);
-            lo = max(lo, lim);
-          }
+          if (rc > cur) hi = min(hi, max(rate_limit(dp.up, true, cur, delta[d]), cur));
+          else if (rc < cur) lo = max(lo, min(rate_limit(dp.dn, false, cur, delta[d]), cur));
           desired = rc < lo ? lo : (rc > hi ? hi : rc);
         }
         // shift history rings; entry 0 = this step
@@ -515,27 +650,28 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         rec[d][0] = ran ? proposal : 0;
         recv[d] = ((recv[d] << 1) | (ran ? 1u : 0u)) & 0xFFu;
         delta[d][0] = (hpa_path && desired != cur) ? desired - cur : 0;
+        if (desired != cur) g_dirty = true;  // PDB expectation changed
         replicas[d] = desired;
       }
       // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d >= D) break;
-        int total = 0;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) total += ni_used(ninfo[n]) ? npods[n][d] : 0;
-        int excess = total - replicas[d];
+        int excess = placed[d] - replicas[d];
         if (excess > 0) {
+          g_dirty = true;
+          placed[d] = replicas[d];
 #pragma unroll
           for (int pass = 0; pass < 2; ++pass) {
+            const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
 #pragma unroll
             for (int n = MAXN - 1; n >= 0; --n) {
-              const bool rdy = nready[n] <= t;
-              if (ni_used(ninfo[n]) && rdy == (pass == 1) && npods[n][d] > 0 && excess > 0) {
+              if ((m >> n & 1u) && npods[n][d] > 0 && excess > 0) {
                 const int k = min(npods[n][d], excess);
                 npods[n][d] -= k;
                 excess -= k;
                 nlast[n] = t;
+                if (pass == 1) rpods[d] -= k;
               }
             }
           }
@@ -543,36 +679,46 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       }
       // ---- E. kube-scheduler (ready) / F1. nomination (in-flight) ----
 #pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
+      for (int d = 0; d < DMAX; ++d) {
+        if (d >= D) break;
+        int pd = replicas[d] - placed[d];
+        if (pd > 0) {
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          if (d >= D) break;
-          int total = 0;
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n) total += ni_used(ninfo[n]) ? npods[n][d] : 0;
-          int pd = replicas[d] - total;
-          if (pd > 0) {
+          for (int pass = 0; pass < 2; ++pass) {
+            const uint32_t m = pass == 0 ? rdy : (used & ~rdy);
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
               const uint32_t x = ninfo[n];
-              const bool rdy = nready[n] <= t;
-              if (pd > 0 && ni_used(x) && rdy == (pass == 0) && (capbit(ni_cap(x)) & capsel[d])) {
-                int sc = 0, sm = 0, sp = 0;
+              if (pd > 0 && (m >> n & 1u) && (capbit(ni_cap(x)) & capsel[d])) {
+                int f;
+                if (DMAX == 1) {
+                  f = ncap[n] - npods[n][0];
+                } else {
+                  int sc = 0, sm = 0, sp = 0;
 #pragma unroll
-                for (int e = 0; e < DMAX; ++e) {
-                  if (e >= D) break;
-                  sc += npods[n][e] * w->deploy[e].req_cpu_m;
-                  sm += npods[n][e] * w->deploy[e].req_mem_mi;
-                  sp += npods[n][e];
+                  for (int e = 0; e < DMAX; ++e) {
+                    if (e >= D) break;
+                    sc += npods[n][e] * dep[e].req_cpu;
+                    sm += npods[n][e] * dep[e].req_mem;
+                    sp += npods[n][e];
+                  }
+                  f = max(type_fit<DMAX>(L, ni_type(x), sc, sm, sp, dep[d].req_cpu, dep[d].req_mem), 0);
                 }
-                const int f = max(type_fit<DMAX>(L, p, ni_type(x), sc, sm, sp, d), 0);
                 const int k = min(f, pd);
-                if (k > 0) { npods[n][d] += k; pd -= k; nlast[n] = t; }
+                if (k > 0) {
+                  npods[n][d] += k;
+                  pd -= k;
+                  placed[d] += k;
+                  nlast[n] = t;
+                  // nominations onto not-ready nodes cannot validate a
+                  // consolidation candidate before readiness (which dirties)
+                  if (pass == 0) { rpods[d] += k; g_dirty = true; }
+                }
               }
             }
           }
-          pend[d] = pd;
         }
+        pend[d] = pd;
       }
     }
 
@@ -581,10 +727,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       int anyp = 0;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) anyp |= pend[d] > 0;
-      uint32_t free_mask = 0;
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) if (!ni_used(ninfo[n]) && n < NN) free_mask |= 1u << n;
-      unsigned long long need = __ballot(active && anyp && free_mask != 0);
+      const uint32_t free_mask = ~used & slot_mask;
+      unsigned long long need = __ballot(active && anyp && free_mask != 0 && !(p.ablate & 2));
       while (need) {
         const int ld = __ffsll((long long)need) - 1;
         need &= need - 1;
@@ -597,11 +741,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         uint32_t lzm[CCKA_MAX_POOLS], lcm[CCKA_MAX_POOLS];
 #pragma unroll
         for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
-          int u = 0;
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n)
-            if (ni_used(ninfo[n]) && ni_pool(ninfo[n]) == q) u += L.types[ni_type(ninfo[n])].vcpu * 1000;
-          use0[q] = rdl(u, ld);
+          use0[q] = rdl(puse[q], ld);
           usenow[q] = use0[q];
           lzm[q] = rdlu(pzm[q], ld);
           lcm[q] = rdlu(pcm[q], ld);
@@ -611,23 +751,24 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         int ncl = 0;
         for (int oi = 0; oi < D; ++oi) {
           const int d = p.prov[oi];
-          int pd_self = 0;
-#pragma unroll
-          for (int e = 0; e < DMAX; ++e) if (e == d) pd_self = pend[e];
-          int rem = rdl(pd_self, ld);
-          if (rem <= 0) continue;
+          int pd_self = 0, rc = 0, rm = 0;
           uint32_t csel_self = 0;
 #pragma unroll
-          for (int e = 0; e < DMAX; ++e) if (e == d) csel_self = capsel[e];
+          for (int e = 0; e < DMAX; ++e)
+            if (e == d) { pd_self = pend[e]; csel_self = capsel[e]; rc = dep[e].req_cpu; rm = dep[e].req_mem; }
+          int rem = rdl(pd_self, ld);
+          if (rem <= 0) continue;
           const uint32_t csel = rdlu(csel_self, ld);
-          const int rc = w->deploy[d].req_cpu_m, rm = w->deploy[d].req_mem_mi;
           for (int c = 0; c < ncl && rem > 0; ++c) {
             int* cl = CL + c * CW;
             const int cpool = cl[0];
             const uint32_t cm = (uint32_t)cl[1] & csel;
             if (!cm) continue;
-            const int j = wave_claim_j<DMAX>(L, p, lrl, (uint32_t)cl[2], cm, cl[4], cl[5], cl[6], d,
-                                             use0[cpool], w->pools[cpool].limit_cpu_m, lane);
+            int climit = 0;
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) climit = plimit[q];
+            const int j = wave_claim_j<DMAX>(L, lrl, (uint32_t)cl[2], cm, cl[4], cl[5], cl[6], rc, rm,
+                                             use0[cpool], climit, lane);
             if (j <= 0) continue;
             const int k = min(j, rem);
             __builtin_amdgcn_wave_barrier();
@@ -645,8 +786,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             for (int q = 0; q < NP; ++q) {
               const uint32_t cm = lcm[q] & csel;
               if (!cm) continue;
-              const int j = wave_claim_j<DMAX>(L, p, lrl, lzm[q], cm, 0, 0, 0, d, use0[q],
-                                               w->pools[q].limit_cpu_m, lane);
+              const int j = wave_claim_j<DMAX>(L, lrl, lzm[q], cm, 0, 0, 0, rc, rm, use0[q], plimit[q], lane);
               if (j > 0) { chosen = q; jj = j; break; }
             }
             if (chosen < 0) break;
@@ -671,31 +811,51 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         for (int c = 0; c < ncl; ++c) {
           const int* cl = CL + c * CW;
           const int cpool = cl[0];
+          int climit = 0;
+#pragma unroll
+          for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) climit = plimit[q];
           const int bi = wave_launch<DMAX>(L, lrl, (uint32_t)cl[2], (uint32_t)cl[1], cl[4], cl[5],
-                                           cl[6], usenow[cpool], w->pools[cpool].limit_cpu_m, lwc,
-                                           lci, lane);
+                                           cl[6], usenow[cpool], climit, lwc, lci, lane);
           if (bi < 0) continue;
           const int bc = bi & 1, bz = (bi >> 1) % Z, bk = (bi >> 1) / Z;
-          usenow[cpool] += L.types[bk].vcpu * 1000;
+          const int vcpu_m = L.types[bk].vcpu * 1000;
+          usenow[cpool] += vcpu_m;
           const int slot = cl[3];
           if (lane == ld) {
             const uint32_t choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)cpool << 16;
+            const bool now_ready = t + delay <= t;
+            const int price = tprice(L, lrl, bk, bz, bc);
+            const int cap = DMAX == 1 ? L.cap1[bk] : 0;
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
               if (n == slot) {
                 ninfo[n] = ni_make(cpool, bk, bz, bc);
-                nready[n] = t + w->provision_delay_steps;
+                nready[n] = t + delay;
                 nlast[n] = t;
+                nprice[n] = price;
+                ncap[n] = cap;
 #pragma unroll
-                for (int e = 0; e < DMAX; ++e) npods[n][e] = e < D ? cl[CLAIM_FIXED + e] : 0;
+                for (int e = 0; e < DMAX; ++e) {
+                  const int k = e < D ? cl[CLAIM_FIXED + e] : 0;
+                  npods[n][e] = k;
+                  placed[e] += k;
+                  if (now_ready) rpods[e] += k;
+                }
               }
             }
-            burn += tprice(L, lrl, bk, bz, bc);
+            used |= 1u << slot;
+            if (now_ready) rdy |= 1u << slot;
+            else next_ready = min(next_ready, t + delay);
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) puse[q] += vcpu_m;
+            if (bc == 0) nsp++; else nod++;
+            burn += price;
             launches++;
             last_choice = choice;
             hash = (hash ^ choice) * 16777619u;
             step_last_type = bk;
             flags |= 2u;
+            if (now_ready) g_dirty = true;
           }
         }
         __builtin_amdgcn_wave_barrier();
@@ -703,133 +863,248 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     }
 
     if (active) {
-      // ---- G. disruption ----
-      long long allowed = 0x3fffffffffffffffLL;
-      if (w->pdb_min_available_pct >= 0) {
-        long long rdy = 0, reps = 0;
+      // ---- G. disruption (skipped exactly when nothing it depends on moved) ----
+      if ((g_dirty || t >= g_wake) && !(p.ablate & 1)) {
+        bool budget_hit = false, any_deleted = false;
+        long long allowed = 0x3fffffffffffffffLL;
+        if (pdb_pct >= 0) {
+          long long rdyp = 0, reps = 0;
 #pragma unroll
-        for (int d = 0; d < DMAX; ++d) {
-          if (d >= D || !w->deploy[d].pdb_member) continue;
-          reps += replicas[d];
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n)
-            if (ni_used(ninfo[n]) && nready[n] <= t) rdy += npods[n][d];
+          for (int d = 0; d < DMAX; ++d) {
+            if (d >= D || !dep[d].pdb) continue;
+            reps += replicas[d];
+            rdyp += rpods[d];
+          }
+          allowed = max(rdyp - ((long long)pdb_pct * reps + 99) / 100, 0LL);
         }
-        allowed = max(rdy - ((long long)w->pdb_min_available_pct * reps + 99) / 100, 0LL);
-      }
-      for (int q = 0; q < NP; ++q) {
-        int npool = 0;
+        for (int q = 0; q < NP; ++q) {
+          int npool = 0, qbudget = 0, qca = 0, qpol = 0;
 #pragma unroll
-        for (int n = 0; n < MAXN; ++n) npool += (ni_used(ninfo[n]) && ni_pool(ninfo[n]) == q) ? 1 : 0;
-        if (npool == 0) continue;
-        const int budget = (w->pools[q].budget_pct * npool + 99) / 100;
-        int deleted = 0;
-        uint32_t rejected = 0;
-        while (deleted < budget) {
-          int best = -1, bpods = 0, bprice = 0;
+          for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+            if (qq == q) { qbudget = pbudget[qq]; qca = pca[qq]; qpol = ppol[qq]; }
 #pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            const uint32_t x = ninfo[n];
-            if (!ni_used(x) || ni_pool(x) != q || nready[n] > t || (rejected >> n & 1u)) continue;
-            if ((t - nlast[n]) * CCKA_STEP_SECONDS < pca[q]) continue;
-            int pods = 0;
+          for (int n = 0; n < MAXN; ++n) npool += ((used >> n & 1u) && ni_pool(ninfo[n]) == q) ? 1 : 0;
+          if (npool == 0) continue;
+          const int budget = (qbudget * npool + 99) / 100;
+          int deleted = 0;
+          if (DMAX == 1) {
+            // identical pods: a candidate's pods fit first-fit on the other
+            // compatible ready nodes iff their free capacities add up, so one
+            // scan over the slots ranks every valid candidate (no rescans per
+            // rejection); the winner is the first valid one in (pods asc, price
+            // desc, slot asc) order, exactly as the spec's sequential search.
+            uint32_t pm = 0, cm1 = 0;
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n][d] : 0;
-            if (pods > 0 && ppol[q] != CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) continue;
-            const int pr = tprice(L, rl, ni_type(x), ni_zone(x), ni_cap(x));
-            if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
-          }
-          if (best < 0) break;
-          bool ok = true;
-          long long pdb_pods = 0;
-          int tpods[MAXN][DMAX];
-          int tlast[MAXN];
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            tlast[n] = nlast[n];
-#pragma unroll
-            for (int d = 0; d < DMAX; ++d) tpods[n][d] = npods[n][d];
-          }
-          if (bpods > 0) {
-            int bp[DMAX];
-#pragma unroll
-            for (int d = 0; d < DMAX; ++d) {
-              bp[d] = 0;
-#pragma unroll
-              for (int n = 0; n < MAXN; ++n) if (n == best) bp[d] = npods[n][d];
-              if (d < D && w->deploy[d].pdb_member) pdb_pods += bp[d];
+            for (int n = 0; n < MAXN; ++n) {
+              const uint32_t x = ninfo[n];
+              if (ni_pool(x) == q) pm |= 1u << n;
+              if (capbit(ni_cap(x)) & capsel[0]) cm1 |= 1u << n;
             }
-            if (pdb_pods > allowed) ok = false;
+            pm &= used;
+            cm1 &= used;
+            while (true) {
+              if (deleted >= budget) { budget_hit = true; break; }
+              int F = 0;
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) {
-              if (d >= D || !ok) break;
-              int need_d = bp[d];
+              for (int n = 0; n < MAXN; ++n) if ((rdy & cm1) >> n & 1u) F += ncap[n] - npods[n][0];
+              int best = -1, bpods = 0, bprice = 0;
 #pragma unroll
               for (int n = 0; n < MAXN; ++n) {
-                const uint32_t x = ninfo[n];
-                if (need_d > 0 && n != best && ni_used(x) && nready[n] <= t && (capbit(ni_cap(x)) & capsel[d])) {
-                  int sc = 0, sm = 0, sp = 0;
+                if (!((pm & rdy) >> n & 1u)) continue;
+                if ((t - nlast[n]) * CCKA_STEP_SECONDS < qca) continue;
+                const int pods = npods[n][0];
+                bool ok = pods == 0;
+                if (!ok && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) {
+                  const int fo = F - ((cm1 >> n & 1u) ? ncap[n] - pods : 0);
+                  ok = fo >= pods && (!dep[0].pdb || (long long)pods <= allowed);
+                }
+                if (!ok) continue;
+                const int pr = nprice[n];
+                if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
+              }
+              if (best < 0) break;
+              int need_d = bpods;
 #pragma unroll
-                  for (int e = 0; e < DMAX; ++e) {
-                    if (e >= D) break;
-                    sc += tpods[n][e] * w->deploy[e].req_cpu_m;
-                    sm += tpods[n][e] * w->deploy[e].req_mem_mi;
-                    sp += tpods[n][e];
-                  }
-                  const int f = max(type_fit<DMAX>(L, p, ni_type(x), sc, sm, sp, d), 0);
-                  const int k = min(f, need_d);
-                  if (k > 0) { tpods[n][d] += k; need_d -= k; tlast[n] = t; }
+              for (int n = 0; n < MAXN; ++n) {
+                if (need_d > 0 && n != best && ((rdy & cm1) >> n & 1u)) {
+                  const int k = min(ncap[n] - npods[n][0], need_d);
+                  if (k > 0) { npods[n][0] += k; need_d -= k; nlast[n] = t; }
                 }
               }
-              if (need_d > 0) ok = false;
-            }
-          }
-          if (!ok) { rejected |= 1u << best; continue; }
 #pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            nlast[n] = tlast[n];
+              for (int n = 0; n < MAXN; ++n) {
+                if (n == best) {
+                  if (ni_cap(ninfo[n]) == 0) nsp--; else nod--;
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) npods[n][d] = tpods[n][d];
-            if (n == best) {
+                  for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+                    if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
+                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+                  npods[n][0] = 0;
+                }
+              }
               burn -= bprice;
-              ninfo[n] = 0; nready[n] = 0; nlast[n] = 0;
-#pragma unroll
-              for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
+              used &= ~(1u << best);
+              rdy &= ~(1u << best);
+              pm &= ~(1u << best);
+              cm1 &= ~(1u << best);
+              if (dep[0].pdb) allowed -= bpods;
+              deleted++;
+              deletions++;
+              any_deleted = true;
+              flags |= 4u;
             }
+            continue;
           }
-          allowed -= pdb_pods;
-          deleted++;
-          deletions++;
-          flags |= 4u;
+          uint32_t rejected = 0;
+          while (true) {
+            if (deleted >= budget) { budget_hit = true; break; }
+            int best = -1, bpods = 0, bprice = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              const uint32_t x = ninfo[n];
+              if (!((rdy & ~rejected) >> n & 1u) || ni_pool(x) != q) continue;
+              if ((t - nlast[n]) * CCKA_STEP_SECONDS < qca) continue;
+              int pods = 0;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n][d] : 0;
+              if (pods > 0 && qpol != CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) continue;
+              const int pr = nprice[n];
+              if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
+            }
+            if (best < 0) break;
+            bool ok = true;
+            long long pdb_pods = 0;
+            if (DMAX == 1) {
+              // identical pods: first-fit succeeds iff the other compatible
+              // ready nodes' free capacities add up to the candidate's pods
+              if (bpods > 0) {
+                if (dep[0].pdb) pdb_pods = bpods;
+                if (pdb_pods > allowed) ok = false;
+                int free_sum = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n)
+                  if (n != best && (rdy >> n & 1u) && (capbit(ni_cap(ninfo[n])) & capsel[0]))
+                    free_sum += ncap[n] - npods[n][0];
+                if (free_sum < bpods) ok = false;
+              }
+              if (!ok) { rejected |= 1u << best; continue; }
+              int need_d = bpods;
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                if (need_d > 0 && n != best && (rdy >> n & 1u) && (capbit(ni_cap(ninfo[n])) & capsel[0])) {
+                  const int k = min(ncap[n] - npods[n][0], need_d);
+                  if (k > 0) { npods[n][0] += k; need_d -= k; nlast[n] = t; }
+                }
+              }
+            } else {
+              int tpods[MAXN][DMAX];
+              int tlast[MAXN];
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                tlast[n] = nlast[n];
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) tpods[n][d] = npods[n][d];
+              }
+              if (bpods > 0) {
+                int bp[DMAX];
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) {
+                  bp[d] = 0;
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) if (n == best) bp[d] = npods[n][d];
+                  if (d < D && dep[d].pdb) pdb_pods += bp[d];
+                }
+                if (pdb_pods > allowed) ok = false;
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) {
+                  if (d >= D || !ok) break;
+                  int need_d = bp[d];
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) {
+                    const uint32_t x = ninfo[n];
+                    if (need_d > 0 && n != best && (rdy >> n & 1u) && (capbit(ni_cap(x)) & capsel[d])) {
+                      int sc = 0, sm = 0, sp = 0;
+#pragma unroll
+                      for (int e = 0; e < DMAX; ++e) {
+                        if (e >= D) break;
+                        sc += tpods[n][e] * dep[e].req_cpu;
+                        sm += tpods[n][e] * dep[e].req_mem;
+                        sp += tpods[n][e];
+                      }
+                      const int f = max(type_fit<DMAX>(L, ni_type(x), sc, sm, sp, dep[d].req_cpu, dep[d].req_mem), 0);
+                      const int k = min(f, need_d);
+                      if (k > 0) { tpods[n][d] += k; need_d -= k; tlast[n] = t; }
+                    }
+                  }
+                  if (need_d > 0) ok = false;
+                }
+              }
+              if (!ok) { rejected |= 1u << best; continue; }
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                nlast[n] = tlast[n];
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) npods[n][d] = tpods[n][d];
+              }
+            }
+            // remove the node (its pods moved between ready nodes: running counts unchanged)
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (n == best) {
+                if (ni_cap(ninfo[n]) == 0) nsp--; else nod--;
+#pragma unroll
+                for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+                  if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
+                ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
+              }
+            }
+            burn -= bprice;
+            used &= ~(1u << best);
+            rdy &= ~(1u << best);
+            allowed -= pdb_pods;
+            deleted++;
+            deletions++;
+            any_deleted = true;
+            flags |= 4u;
+          }
         }
+        g_dirty = budget_hit || any_deleted;
+        // next step at which a node becomes a new candidate (consolidatable and ready)
+        int wake = 0x7fffffff;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) {
+          if (used >> n & 1u) {
+            int ca = 0;
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == ni_pool(ninfo[n])) ca = pca[q];
+            const int thr = max(nready[n], nlast[n] + (ca + CCKA_STEP_SECONDS - 1) / CCKA_STEP_SECONDS);
+            if (thr > t) wake = min(wake, thr);
+          }
+        }
+        g_wake = wake;
       }
       // ---- H. accounting ----
-      int ready_d[DMAX];
       double upp[DMAX];
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        ready_d[d] = 0;
         upp[d] = 0.0;
         if (d >= D) continue;
-        int rd = 0;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) if (ni_used(ninfo[n]) && nready[n] <= t) rd += npods[n][d];
-        ready_d[d] = rd;
+        const int rd = rpods[d];
         if (rd > 0) {
-          long long usage = Lt[d];
-          if (w->deploy[d].limit_cpu_m > 0) usage = min(usage, (long long)rd * w->deploy[d].limit_cpu_m);
+          long long usage = Lcur[d];
+          if (dep[d].limit > 0) usage = min(usage, (long long)rd * dep[d].limit);
           upp[d] = (double)usage / (double)rd;
         }
       }
       double step_w = base_w;
-      int nsp = 0, nod = 0;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        const uint32_t x = ninfo[n];
-        if (!ni_used(x)) continue;
-        const ccka_itype& ty = L.types[ni_type(x)];
+        if (!(used >> n & 1u) || (p.ablate & 4)) continue;
+        const ccka_itype& ty = L.types[ni_type(ninfo[n])];
         double u = 0.0;
-        if (nready[n] <= t) {
+        if (rdy >> n & 1u) {
           double xs = 0.0;
 #pragma unroll
           for (int d = 0; d < DMAX; ++d) if (d < D) xs += (double)npods[n][d] * upp[d];
@@ -837,7 +1112,6 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           if (u > 1.0) u = 1.0;
         }
         step_w += ty.p_idle_w + ty.p_dyn_w * u;
-        if (ni_cap(x) == 0) nsp++; else nod++;
       }
       cost += burn + base_price;
       energy += step_w;
@@ -847,11 +1121,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d >= D) continue;
-        pending += replicas[d] - ready_d[d];
+        pending += replicas[d] - rpods[d];
         reps += replicas[d];
-        const ccka_deployment& dp = w->deploy[d];
-        if (dp.scaler == CCKA_SCALER_HPA && util_valid[d] && util[d] > w->slo_util_pct) viol = true;
-        if (dp.scaler == CCKA_SCALER_KEDA && (long long)Lt[d] > dp.keda_activation && replicas[d] == 0) viol = true;
+        if (dep[d].scaler == CCKA_SCALER_HPA && util_valid[d] && util[d] > slo_util) viol = true;
+        if (dep[d].scaler == CCKA_SCALER_KEDA && (long long)Lcur[d] > dep[d].kact && replicas[d] == 0) viol = true;
       }
       if (pending > 0) viol = true;
       if (viol) { slo++; flags |= 8u; }
@@ -872,11 +1145,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     }
   }
   if (!active) return;
-  int reps = 0, nodes = 0;
+  int reps = 0;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) reps += d < D ? replicas[d] : 0;
-#pragma unroll
-  for (int n = 0; n < MAXN; ++n) nodes += ni_used(ninfo[n]);
   p.cost[i] = cost;
   p.energy[i] = energy;
   p.gco2[i] = gco2;
@@ -888,7 +1159,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   p.deletions[i] = deletions;
   p.peak_nodes[i] = peak_nodes;
   p.final_reps[i] = reps;
-  p.final_nodes[i] = nodes;
+  p.final_nodes[i] = __popc(used);
   p.last_choice[i] = last_choice;
   p.hash[i] = hash;
 }
