@@ -103,6 +103,7 @@ def main():
     # max i16, cap_sel u8 = 6 B) read once, results (4x8 + 10x4 = 72 B) written once
     bytes_launch = N * T * 4 + (N * T * 16 if traj else 0) + N * 6 + N * 72
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+    traffic = measured_traffic(args.mode, N, T)
     out = {
         "metric": "policy-evaluated cluster-steps/sec",
         "value": value,
@@ -121,7 +122,7 @@ def main():
                    "scenarios_per_gpu": N, "steps_per_rollout": T, "mode": args.mode,
                    "parallelism": f"scenario-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "rollout_kernel<1,8>", "kernel_ms_avg": avg_ms,
                      "bytes_per_launch": bytes_launch},
         "totals": {"cost_usd": totals.cost_uphmin / 6e7, "energy_kwh": totals.energy_wmin / 6e4,
@@ -135,6 +136,20 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def measured_traffic(mode, n, T):
+    """HBM bytes per launch of the rollout kernel measured by rocprofv3 PMC
+    passes of this same command (tools/prof_round.sh; L2 memory-side request
+    counters TCC_EA0_RDREQ_{32,64,128}B x size + TCC_EA0_WRREQ_64B x 64), kept
+    under profiles/. None when no profile matches this workload."""
+    import glob
+
+    name = "config2_traj_summary.json" if mode == "trajectory" else "config2_summary_summary.json"
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*", name)))
+    if not paths or (n, T) != (100_000, 1440):
+        return None
+    return json.load(open(paths[-1])).get("traffic_bytes")
 
 
 def cpu_baseline(eng, spec, sc, target_s):

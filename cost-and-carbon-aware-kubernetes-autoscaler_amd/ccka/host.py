@@ -1,0 +1,110 @@
+"""ctypes binding of libccka_host.so (include/ccka_host.h): manifest ingest,
+kubectl apply/patch emulation, the reference scripts' payload generators, and
+the manifest -> ccka_world builder. No GPU needed."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import abi
+
+HOST_LIB = os.path.join(os.path.dirname(abi.PKG_DIR), "host", "build", "libccka_host.so")
+CLI = os.path.join(os.path.dirname(abi.PKG_DIR), "host", "build", "ccka")
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(HOST_LIB):
+            raise abi.CckaError(f"host library not built: {HOST_LIB}")
+        L = C.CDLL(HOST_LIB)
+        vp = C.c_void_p
+        sig = {
+            "ccka_host_open": (C.c_int, [C.POINTER(vp)]),
+            "ccka_host_close": (None, [vp]),
+            "ccka_host_last_error": (C.c_char_p, [vp]),
+            "ccka_host_apply": (C.c_int, [vp, C.c_char_p]),
+            "ccka_host_patch": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p]),
+            "ccka_host_get_json": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int64]),
+            "ccka_host_policy_patch": (C.c_int, [vp, C.c_int32, C.c_char_p, C.c_int32, C.c_int32,
+                                                 C.c_char_p, C.c_int64]),
+            "ccka_host_burst_manifest": (C.c_int, [vp, C.c_int32, C.c_char_p, C.c_int64]),
+            "ccka_host_build_world": (C.c_int, [vp, C.c_char_p, C.c_int32, C.c_int32,
+                                                C.POINTER(abi.World)]),
+            "ccka_host_summary": (C.c_int, [vp, C.POINTER(abi.World), C.POINTER(abi.Results),
+                                            C.POINTER(abi.TrajRec), C.c_char_p, C.c_int64]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+HOST_EXPORTED = ["ccka_host_open", "ccka_host_close", "ccka_host_last_error", "ccka_host_apply",
+                 "ccka_host_patch", "ccka_host_get_json", "ccka_host_policy_patch",
+                 "ccka_host_burst_manifest", "ccka_host_build_world", "ccka_host_summary"]
+
+
+class Host:
+    """One manifest store. Environment (NP_SPOT, OFFPEAK_ZONES, ...) is read at open."""
+
+    def __init__(self):
+        self.L = lib()
+        self.h = C.c_void_p()
+        abi.check(self.L.ccka_host_open(C.byref(self.h)), "ccka_host_open")
+        self._buf = C.create_string_buffer(1 << 20)
+
+    def close(self):
+        if self.h:
+            self.L.ccka_host_close(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, what):
+        raise abi.CckaError(f"{what}: {self.L.ccka_host_last_error(self.h).decode()}")
+
+    def _str(self, n, what):
+        if n < 0:
+            self._err(what)
+        return self._buf.raw[:n].decode()
+
+    def apply(self, yaml_text: str):
+        if self.L.ccka_host_apply(self.h, yaml_text.encode()) != 0:
+            self._err("apply")
+
+    def patch(self, kind, name, ptype, text):
+        if self.L.ccka_host_patch(self.h, kind.encode(), name.encode(), ptype.encode(), text.encode()) != 0:
+            self._err("patch")
+
+    def get_json(self, kind, name) -> str:
+        return self._str(self.L.ccka_host_get_json(self.h, kind.encode(), name.encode(), self._buf,
+                                                   len(self._buf)), "get_json")
+
+    def policy_patch(self, profile: int, pool: str, json_patch: bool, fallback=False) -> str:
+        return self._str(self.L.ccka_host_policy_patch(self.h, profile, pool.encode(), int(json_patch),
+                                                       int(fallback), self._buf, len(self._buf)),
+                         "policy_patch")
+
+    def manifest(self, index: int) -> str:
+        return self._str(self.L.ccka_host_burst_manifest(self.h, index, self._buf, len(self._buf)),
+                         "manifest")
+
+    def build_world(self, catalog="tiny", n_steps=1440, max_nodes=16) -> abi.World:
+        w = abi.World()
+        if self.L.ccka_host_build_world(self.h, catalog.encode(), n_steps, max_nodes, C.byref(w)) != 0:
+            self._err("build_world")
+        return w
+
+    def summary(self, world, results, traj=None) -> str:
+        tp = traj.ctypes.data_as(C.POINTER(abi.TrajRec)) if traj is not None else None
+        return self._str(self.L.ccka_host_summary(self.h, C.byref(world), C.byref(results), tp,
+                                                  self._buf, len(self._buf)), "summary")

@@ -1,0 +1,67 @@
+/*
+ * ccka_host.h — C ABI of libccka_host.so: the manifest-in / summary-out side
+ * of the drop-in (no GPU needed).
+ *
+ * It replaces the kubectl round-trips of the reference's decision path:
+ *   ccka_host_apply         `kubectl apply -f`            demo_30_burst_configure.sh:143,
+ *                                                          demo_10_setup_configure.sh (PDB, RBAC)
+ *   ccka_host_patch         `kubectl patch --type=merge|json`
+ *                                                          demo_20_offpeak_configure.sh:59-60,96;
+ *                                                          demo_21_peak_configure.sh:56-57,88;
+ *                                                          demo_19_reset_policies.sh:68-75
+ *   ccka_host_get_json      `kubectl get nodepool -o json` (the read-back of apply_and_verify,
+ *                                                          demo_20_offpeak_configure.sh:102)
+ *   ccka_host_policy_patch  write_req_patch + the merge patches (demo_20 :59-81, demo_21 :56-77,
+ *                           demo_19 :68-75), byte-identical to what the scripts send
+ *   ccka_host_burst_manifest demo_30_burst_configure.sh:78-141 heredoc, byte-identical
+ *   ccka_host_build_world   the stored objects -> ccka_world for libccka (ccka.h)
+ *   ccka_host_summary       the missing demo_41_observe_cost_nodes.sh (README.md:57)
+ * Environment names follow the scripts: NP_SPOT, NP_OD, OFFPEAK_ZONES,
+ * PEAK_ZONES, NAMESPACE, COUNT, REPLICAS (demo_00_env.sh, demo_30 :7-8),
+ * with the same ${VAR:-default} rules, read at ccka_host_open.
+ *
+ * Strings out: the call writes at most `cap` bytes including the NUL and
+ * returns the length written (>= 0), or a negative ccka_status.
+ */
+#ifndef CCKA_HOST_H
+#define CCKA_HOST_H
+
+#include <stdint.h>
+
+#include "ccka.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ccka_host ccka_host;
+
+int ccka_host_open(ccka_host** out);
+void ccka_host_close(ccka_host* h);
+const char* ccka_host_last_error(const ccka_host* h);
+
+int ccka_host_apply(ccka_host* h, const char* yaml);
+int ccka_host_patch(ccka_host* h, const char* kind, const char* name, const char* type,
+                    const char* patch);
+int ccka_host_get_json(ccka_host* h, const char* kind, const char* name, char* out, int64_t cap);
+
+/* profile: CCKA_PROFILE_*; json_patch 0 -> the merge patch, 1 -> the
+ * requirements JSON Patch (fallback 1: /spec/template path) */
+int ccka_host_policy_patch(ccka_host* h, int32_t profile, const char* pool, int32_t json_patch,
+                           int32_t fallback, char* out, int64_t cap);
+/* index >= 1: that Deployment; 0: the PodDisruptionBudget; -1: the base NodePools */
+int ccka_host_burst_manifest(ccka_host* h, int32_t index, char* out, int64_t cap);
+
+/* catalog: "tiny" (12 types) or "small" (16). The world's array pointers
+ * stay valid until the next build or ccka_host_close. */
+int ccka_host_build_world(ccka_host* h, const char* catalog, int32_t n_steps, int32_t max_nodes,
+                          ccka_world* out);
+/* demo_41-style summary of scenario 0 (results arrays of length >= 1;
+ * traj may be NULL) */
+int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
+                      const ccka_traj_rec* traj, char* out, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -90,3 +90,20 @@ def totals(arrays, n):
     t = abi.Totals()
     lib().ccka_oracle_totals(C.byref(r), n, C.byref(t))
     return t
+
+
+def rollout_world(world, scen, load, traj=False, threads=1):
+    """Like rollout() but from a raw abi.World (e.g. built by libccka_host)."""
+    s = scen.to_c()
+    load = np.ascontiguousarray(load, np.int32)
+    arrays, r = alloc_results(scen.n)
+    tr = None
+    trp = None
+    if traj:
+        tr = np.zeros((world.n_steps, scen.n), TRAJ_DTYPE)
+        trp = tr.ctypes.data_as(C.POINTER(abi.TrajRec))
+    rc = lib().ccka_oracle_rollout(C.byref(world), C.byref(s), load.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   C.byref(r), trp, threads)
+    if rc != 0:
+        raise abi.CckaError(f"oracle rollout failed: {rc}")
+    return arrays, tr
