@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 STEP_SECONDS = 60
 MAX_TYPES = 1024
 MAX_ZONES = 4
@@ -31,8 +31,8 @@ STATUS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ERCCL",
 
 class ItType(C.Structure):
     _fields_ = [("vcpu", C.c_int32), ("alloc_cpu_m", C.c_int32), ("alloc_mem_mi", C.c_int32),
-                ("max_pods", C.c_int32), ("p_idle_w", C.c_double), ("p_dyn_w", C.c_double),
-                ("p_ref_w", C.c_double), ("inv_alloc_cpu", C.c_double)]
+                ("max_pods", C.c_int32), ("idle_nw", C.c_int64), ("dyn_nw_per_m", C.c_int64),
+                ("p_ref_w", C.c_double), ("_reserved", C.c_double)]
 
 
 class PoolPatch(C.Structure):

@@ -92,6 +92,19 @@ class Engine:
         self._chk(self.lib.ccka_get_totals(self.ctx, C.byref(t)), "ccka_get_totals")
         return t
 
+    def set_engine(self, mode: int):
+        """Internal: 0 = automatic engine choice, 1 = general kernel only."""
+        self.lib.ccka_debug_engine.argtypes = [C.c_void_p, C.c_int32]
+        self._chk(self.lib.ccka_debug_engine(self.ctx, mode), "ccka_debug_engine")
+
+    def last_engine(self):
+        """Internal: (engine, table_ms) of the last rollout; engine 1 = general
+        kernel, 2 = single-deployment kernel (rollout_d1.hip)."""
+        e, ms = C.c_int32(), C.c_double()
+        self._chk(self.lib.ccka_debug_last_engine(self.ctx, C.byref(e), C.byref(ms)),
+                  "ccka_debug_last_engine")
+        return e.value, ms.value
+
     def device_info(self):
         name = C.create_string_buffer(256)
         cus = C.c_int32()

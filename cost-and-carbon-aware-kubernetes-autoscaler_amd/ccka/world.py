@@ -39,6 +39,12 @@ NP_SPOT = "spot-preferred"
 NP_OD = "on-demand-slo"
 
 
+def llround(x: float) -> int:
+    """C llround: nearest integer, halves away from zero."""
+    import math
+    return int(math.copysign(math.floor(abs(x) + 0.5), x))
+
+
 def zone_bit(zone: str) -> int:
     """'us-east-2a' -> bit 0, 'b' -> bit 1, ..."""
     return 1 << (ord(zone.strip()[-1]) - ord("a"))
@@ -107,10 +113,11 @@ class Catalog:
             t.alloc_cpu_m = int(ac[i])
             t.alloc_mem_mi = int(am[i])
             t.max_pods = int(self.max_pods[i])
-            t.p_idle_w = float(v) * W_MIN_PER_VCPU * PUE
-            t.p_dyn_w = float(v) * (W_MAX_PER_VCPU - W_MIN_PER_VCPU) * PUE
-            t.p_ref_w = t.p_idle_w + 0.5 * t.p_dyn_w
-            t.inv_alloc_cpu = 1.0 / float(t.alloc_cpu_m)
+            p_idle = float(v) * W_MIN_PER_VCPU * PUE
+            p_dyn = float(v) * (W_MAX_PER_VCPU - W_MIN_PER_VCPU) * PUE
+            t.idle_nw = llround(p_idle * 1e9)
+            t.dyn_nw_per_m = llround(p_dyn * 1e9 / float(t.alloc_cpu_m))
+            t.p_ref_w = p_idle + 0.5 * p_dyn
         return arr
 
     def index(self, name):

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -26,7 +27,7 @@ using namespace ccka;
 struct ccka_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev_mid = nullptr, ev1 = nullptr;  // ev_mid: after the argmin tables
   std::string err;
   int cus = 0;
   char name[128] = {0};
@@ -64,8 +65,30 @@ struct ccka_ctx {
   ccka_totals* d_totals = nullptr;
   int32_t* d_sinq = nullptr;
   ncclComm_t comm = nullptr;
-  double last_ms = 0.0;
+  double last_ms = 0.0;        // rollout kernel (HIP events on the engine stream)
+  double last_table_ms = 0.0;  // argmin-table kernel of the same rollout
   bool ran = false;
+  // single-deployment engine (rollout_d1.hip): world digest, argmin tables
+  bool d1_world = false;     // the world qualifies (d1_check_world)
+  bool d1_ready = false;     // scenario-dependent part prepared
+  bool d1_ok = false;        // world + scenarios qualify
+  bool sc_maxr_ok = true;
+  D1Params d1{};
+  std::vector<uint32_t> zmasks;
+  std::vector<double> h_cw;  // per-scenario carbon weights (empty: world default)
+  long long* d_acc = nullptr;
+  int32_t* d_order = nullptr;
+  int32_t* d_cap1s = nullptr;
+  uint32_t* d_zmasks = nullptr;
+  double* d_wc1000 = nullptr;
+  uint8_t* d_wci = nullptr;
+  int2* d_table = nullptr;
+  int32_t* d_jtab = nullptr;
+  int JT = 0, NW = 0;
+  int engine_mode = 0;       // 0 auto, 1 general kernel only (ccka_debug_engine)
+  unsigned long long* d_stamps = nullptr;
+  int lpw = 64;              // scenarios per wave of the single-deployment kernel
+  int last_engine = 0;       // 1 general, 2 single-deployment
 };
 
 static int fail(ccka_ctx* c, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -103,6 +126,175 @@ static int dupload(ccka_ctx* c, T*& dst, const T* src, size_t count) {
   return CCKA_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// Single-deployment engine: eligibility and world digest.
+// Conditions (anything else runs the general kernel): one HPA Deployment, no
+// NodePool CPU limits (the launch choice is then independent of pool usage),
+// replica counts and records within int16, tolerance in [0, 1), at most
+// D1_MAX_ZI distinct zone masks and D1_MAX_WC distinct carbon weights.
+// ---------------------------------------------------------------------------
+static int pod_cap(const ccka_itype& t, int rc, int rm) {
+  int f = t.max_pods;
+  if (rc > 0) f = std::min(f, t.alloc_cpu_m / rc);
+  if (rm > 0) f = std::min(f, t.alloc_mem_mi / rm);
+  return f;
+}
+
+static D1Rule d1_rule(const ccka_hpa_rules& r, bool up) {
+  auto wm = [](int w) {
+    int m = 0;
+    for (int k = 0; k < CCKA_HIST; ++k) m |= ((k + 1) * CCKA_STEP_SECONDS < w) ? (1 << k) : 0;
+    return m;
+  };
+  D1Rule o{};
+  o.sel = r.select;
+  o.n = r.n_policies;
+  o.stab_mask = wm(r.stab_window_s);
+  for (int q = 0; q < 2; ++q) {
+    o.type[q] = r.policies[q].type;
+    o.value[q] = r.policies[q].value;
+    o.pmask[q] = wm(r.policies[q].period_s);
+    o.factor[q] = up ? (1.0 + (double)o.value[q] / 100.0) : (1.0 - (double)o.value[q] / 100.0);
+  }
+  for (int r = 0; r < 4; ++r) {
+    auto bit = [](int m, int e) { return (m >> e) & 1; };
+    o.stab16[r] = (bit(o.stab_mask, 2 * r) ? 0xFFFF : 0) | (bit(o.stab_mask, 2 * r + 1) ? (int32_t)0xFFFF0000 : 0);
+    for (int q = 0; q < 2; ++q) {
+      const int m = q < o.n ? o.pmask[q] : 0;
+      o.pm16[q][r] = (bit(m, 2 * r) ? 1 : 0) | (bit(m, 2 * r + 1) ? 0x10000 : 0);
+    }
+  }
+  return o;
+}
+
+static int d1_check_world(ccka_ctx* c) {
+  const ccka_world& w = c->hw;
+  c->d1_world = false;
+  c->d1_ready = false;
+  const ccka_deployment& dp = w.deploy[0];
+  if (w.n_deploy != 1 || dp.scaler != CCKA_SCALER_HPA) return CCKA_OK;
+  for (int q = 0; q < w.n_pools; ++q)
+    if (w.pools[q].limit_cpu_m >= 0) return CCKA_OK;
+  if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
+      dp.min_replicas < 0 || dp.max_replicas < 0 || dp.max_replicas > D1_REC_SAT || dp.replicas0 > D1_REC_SAT)
+    return CCKA_OK;
+  const int K = w.n_types;
+  std::vector<int> cap1(K);
+  int jmax = 0;
+  for (int k = 0; k < K; ++k) {
+    cap1[k] = std::max(0, pod_cap(w.types[k], dp.req_cpu_m, dp.req_mem_mi));
+    if (cap1[k] > D1_REC_SAT || w.types[k].alloc_cpu_m >= (1 << 24) || w.types[k].idle_nw < 0 ||
+        w.types[k].dyn_nw_per_m < 0 || w.types[k].dyn_nw_per_m > 0xFFFFFFFFLL)
+      return CCKA_OK;
+    jmax = std::max(jmax, cap1[k]);
+  }
+  // distinct zone masks of every patch that sets one
+  std::vector<uint32_t> zm;
+  auto zidx = [&](uint32_t m) -> int {
+    if (!m) return -1;
+    for (size_t i = 0; i < zm.size(); ++i) if (zm[i] == m) return (int)i;
+    zm.push_back(m);
+    return (int)zm.size() - 1;
+  };
+  D1Params& p = c->d1;
+  p = D1Params{};
+  for (int q = 0; q < w.n_pools; ++q) {
+    const ccka_pool_patch* src[4] = {&w.pools[q].base, &w.pools[q].profile[CCKA_PROFILE_RESET],
+                                     &w.pools[q].profile[CCKA_PROFILE_OFFPEAK], &w.pools[q].profile[CCKA_PROFILE_PEAK]};
+    for (int s = 0; s < 4; ++s) {
+      D1Patch& x = p.patch[q][s];
+      x.policy = src[s]->policy;
+      const int ca = src[s]->consolidate_after_s;
+      x.cas = ca >= 0 ? (ca + CCKA_STEP_SECONDS - 1) / CCKA_STEP_SECONDS : -1;
+      x.zi = zidx(src[s]->zone_mask & ((1u << w.n_zones) - 1u));
+      x.cm = (int32_t)(src[s]->cap_mask & 3u);
+    }
+    p.budget[q] = w.pools[q].budget_pct;
+  }
+  if (zm.empty()) zm.push_back(1u);  // no pool ever selects a zone: J = 0 everywhere
+  if ((int)zm.size() > D1_MAX_ZI) return CCKA_OK;
+  // accounting coefficients and the catalog in pod-capacity-descending order
+  std::vector<long long> acc((size_t)K * 3);
+  std::vector<int32_t> order(K), cap1s(K);
+  for (int k = 0; k < K; ++k) {
+    acc[(size_t)k * 3 + 0] = w.types[k].idle_nw;
+    acc[(size_t)k * 3 + 1] = w.types[k].dyn_nw_per_m;
+    acc[(size_t)k * 3 + 2] = w.types[k].alloc_cpu_m;
+    order[k] = k;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cap1[a] > cap1[b]; });
+  for (int k = 0; k < K; ++k) cap1s[k] = cap1[order[k]];
+  int rc;
+  if ((rc = dupload(c, c->d_acc, acc.data(), acc.size())) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_order, order.data(), order.size())) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_cap1s, cap1s.data(), cap1s.size())) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_zmasks, zm.data(), zm.size())) != CCKA_OK) return rc;
+  c->zmasks = zm;
+  c->JT = jmax + 1;
+  p.T = w.n_steps; p.K = K; p.Z = w.n_zones; p.R = w.n_regions; p.NP = w.n_pools; p.maxn = w.max_nodes;
+  p.NZI = (int)zm.size(); p.JT = c->JT;
+  p.start_minute = w.start_minute; p.peak_start = w.peak_start_min; p.peak_end = w.peak_end_min;
+  p.pswitch0 = w.peak_switch; p.delay = w.provision_delay_steps;
+  p.base_nodes = w.base_nodes; p.base_type = w.base_type; p.slo_util = w.slo_util_pct;
+  p.pdb_pct = w.pdb_min_available_pct; p.pdb_member = dp.pdb_member ? 1 : 0;
+  p.replicas0 = dp.replicas0; p.minr = dp.min_replicas; p.maxr0 = dp.max_replicas;
+  p.target0 = dp.target_util_pct; p.req_cpu = dp.req_cpu_m; p.limit = dp.limit_cpu_m;
+  p.dstab0 = dp.down.stab_window_s; p.reset_ca0 = w.reset_ca_s; p.capsel0 = (int32_t)dp.cap_sel;
+  p.tol_lo = 1.0 - dp.tolerance;
+  p.tol_hi = 1.0 + dp.tolerance;
+  const ccka_itype& bt = w.types[w.base_type];
+  p.base_nw = (long long)w.base_nodes *
+              (bt.idle_nw + bt.dyn_nw_per_m * (long long)(w.base_util * (double)bt.alloc_cpu_m));
+  p.up = d1_rule(dp.up, true);
+  p.dn = d1_rule(dp.down, false);
+  c->d1_world = true;
+  return CCKA_OK;
+}
+
+// scenario-dependent part: distinct carbon weights, per-scenario index, tables
+static int d1_prepare(ccka_ctx* c) {
+  c->d1_ready = true;
+  c->d1_ok = false;
+  if (!c->d1_world || !c->sc_maxr_ok) return CCKA_OK;
+  const size_t n = (size_t)c->N;
+  std::vector<double> wl;
+  std::vector<uint8_t> wci;
+  if (!c->h_cw.empty()) {
+    std::map<uint64_t, int> seen;
+    wci.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t b;
+      std::memcpy(&b, &c->h_cw[i], 8);
+      auto it = seen.find(b);
+      if (it == seen.end()) {
+        if ((int)wl.size() >= D1_MAX_WC) return CCKA_OK;
+        it = seen.emplace(b, (int)wl.size()).first;
+        wl.push_back(c->h_cw[i]);
+      }
+      wci[i] = (uint8_t)it->second;
+    }
+  } else {
+    wl.push_back(c->hw.carbon_weight);
+  }
+  std::vector<double> wc1000(wl.size());
+  for (size_t k = 0; k < wl.size(); ++k) wc1000[k] = wl[k] * 1000.0;
+  int rc;
+  if ((rc = dupload(c, c->d_wc1000, wc1000.data(), wc1000.size())) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_wci, wci.empty() ? nullptr : wci.data(), wci.size())) != CCKA_OK) return rc;
+  c->NW = (int)wl.size();
+  const ccka_world& w = c->hw;
+  const size_t keys = (size_t)w.n_regions * 24 * c->zmasks.size() * 3;
+  dfree(c->d_table);
+  dfree(c->d_jtab);
+  if (hipMalloc((void**)&c->d_table, keys * c->NW * c->JT * sizeof(int2)) != hipSuccess ||
+      hipMalloc((void**)&c->d_jtab, keys * sizeof(int32_t)) != hipSuccess)
+    return fail(c, CCKA_ENOMEM, "argmin table alloc (%zu keys x %d weights x %d)", keys, c->NW, c->JT);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->d1_ok = true;
+  return CCKA_OK;
+}
+
 extern "C" {
 
 int32_t ccka_abi_version(void) { return CCKA_ABI_VERSION; }
@@ -135,7 +327,8 @@ int ccka_open(ccka_ctx** out, int device_ordinal) {
   c->cus = prop.multiProcessorCount;
   std::snprintf(c->name, sizeof c->name, "%s (%s)", prop.name, prop.gcnArchName);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev_mid) != hipSuccess) {
     delete c;
     return CCKA_EHIP;
   }
@@ -167,9 +360,12 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_region); dfree(c->d_target); dfree(c->d_maxr); dfree(c->d_dstab); dfree(c->d_resetca);
   dfree(c->d_pswitch); dfree(c->d_cw); dfree(c->d_capsel); dfree(c->d_load); dfree(c->d_totals);
   dfree(c->d_sinq);
+  dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
+  dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev_mid) (void)hipEventDestroy(c->ev_mid);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -235,6 +431,7 @@ int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
     if (A.req_cpu_m != B.req_cpu_m) return A.req_cpu_m > B.req_cpu_m;
     return A.req_mem_mi > B.req_mem_mi;
   });
+  if ((rc = d1_check_world(c)) != CCKA_OK) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_world = true;
   c->have_load = false;
@@ -306,6 +503,13 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   if ((rc = dupload(c, c->d_cw, sc->carbon_weight, n)) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_capsel, sc->cap_sel, n)) != CCKA_OK) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->h_cw.clear();
+  if (sc->carbon_weight) c->h_cw.assign(sc->carbon_weight, sc->carbon_weight + n);
+  c->sc_maxr_ok = true;
+  if (sc->max_replicas)
+    for (size_t i = 0; i < n; ++i)
+      if (sc->max_replicas[i] < 0) { c->sc_maxr_ok = false; break; }
+  c->d1_ready = false;
   c->N = sc->n;
   c->first_id = sc->first_id;
   if ((rc = alloc_results(c)) != CCKA_OK) return rc;
@@ -459,9 +663,48 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
   k.P = w.n_pools;
   k.maxn = w.max_nodes;
   for (int d = 0; d < CCKA_MAX_DEPLOY; ++d) k.prov[d] = c->prov[d];
-  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  HIPCHK(c, launch_rollout(k, block, lds, c->stream));
-  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  if (c->engine_mode == 0 && c->d1_world && !c->d1_ready && (rc = d1_prepare(c)) != CCKA_OK) return rc;
+  if (c->engine_mode == 0 && c->d1_world && c->d1_ok) {
+    // single-deployment engine: argmin tables for this rollout, then the rollout
+    TableParams tp{};
+    tp.price = c->d_price; tp.ci_gpwh = c->d_ci_gpwh; tp.types = c->d_types;
+    tp.order = c->d_order; tp.cap1s = c->d_cap1s; tp.zmasks = c->d_zmasks; tp.wc1000 = c->d_wc1000;
+    tp.table = c->d_table; tp.jtab = c->d_jtab;
+    tp.K = w.n_types; tp.Z = w.n_zones; tp.R = w.n_regions; tp.NZI = (int)c->zmasks.size();
+    tp.NW = c->NW; tp.JT = c->JT;
+    D1Params& p = c->d1;
+    p.load = c->d_load; p.price = c->d_price; p.ci_gpwmin = c->d_ci_gpwmin; p.acc = c->d_acc;
+    p.table = c->d_table; p.jtab = c->d_jtab;
+    p.region = c->d_region; p.target = c->d_target; p.maxr = c->d_maxr; p.down_stab = c->d_dstab;
+    p.reset_ca = c->d_resetca; p.pswitch = c->d_pswitch; p.wci = c->d_wci; p.cap_sel = c->d_capsel;
+    p.cost = k.cost; p.energy = k.energy; p.gco2 = k.gco2; p.slo = k.slo; p.pend_min = k.pend_min;
+    p.nmin_spot = k.nmin_spot; p.nmin_od = k.nmin_od; p.launches = k.launches; p.deletions = k.deletions;
+    p.peak_nodes = k.peak_nodes; p.final_reps = k.final_reps; p.final_nodes = k.final_nodes;
+    p.last_choice = k.last_choice; p.hash = k.hash; p.traj = k.traj;
+    p.N = c->N;
+    p.NW = c->NW;
+    p.lpw = c->lpw;
+    p.ablate = k.ablate;
+    p.stamps = nullptr;
+    if (k.ablate & 16) {  // diagnostic phase stamps (single-deployment engine, 8 slots, 2 pools)
+      if (!c->d_stamps && hipMalloc((void**)&c->d_stamps, 12 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "stamps alloc");
+      HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, 12 * sizeof(unsigned long long), c->stream));
+      p.stamps = c->d_stamps;
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, launch_table(tp, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
+    HIPCHK(c, launch_rollout_d1(p, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->last_engine = 2;
+  } else {
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
+    HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->last_engine = 1;
+  }
   c->traj_valid = trajectory != 0;
   c->ran = true;
   return CCKA_OK;
@@ -472,9 +715,11 @@ int ccka_sync(ccka_ctx* c) {
   (void)hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->ran) {
-    float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    float ms = 0.f, tab = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_mid, c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&tab, c->ev0, c->ev_mid));
     c->last_ms = ms;
+    c->last_table_ms = tab;
   }
   return CCKA_OK;
 }
@@ -584,6 +829,37 @@ int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
 int ccka_debug_ablate(ccka_ctx* c, int32_t mask) {
   if (!c) return CCKA_EINVAL;
   c->kp.ablate = mask;
+  return CCKA_OK;
+}
+
+// Internal (not in include/ccka.h): 0 = choose the engine automatically,
+// 1 = always the general kernel (tests compare both engines).
+int ccka_debug_engine(ccka_ctx* c, int32_t mode) {
+  if (!c || mode < 0 || mode > 1) return CCKA_EINVAL;
+  c->engine_mode = mode;
+  return CCKA_OK;
+}
+
+// Internal: which engine ran last (1 general, 2 single-deployment) and the
+// duration of its argmin-table kernel.
+int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
+  if (!c) return CCKA_EINVAL;
+  if (engine) *engine = c->last_engine;
+  if (table_ms) *table_ms = c->last_table_ms;
+  return CCKA_OK;
+}
+
+// Internal: scenarios per wave of the single-deployment kernel (1..64).
+int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
+  if (!c || lpw < 1 || lpw > 64) return CCKA_EINVAL;
+  c->lpw = lpw;
+  return CCKA_OK;
+}
+
+// Internal: per-phase cycle totals of the last stamped rollout (ablate bit 16).
+int ccka_debug_stamps(ccka_ctx* c, unsigned long long* out8) {
+  if (!c || !out8 || !c->d_stamps) return CCKA_EINVAL;
+  HIPCHK(c, hipMemcpy(out8, c->d_stamps, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return CCKA_OK;
 }
 

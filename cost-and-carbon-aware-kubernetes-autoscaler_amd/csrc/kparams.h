@@ -85,4 +85,94 @@ hipError_t launch_gen_load(const GenParams& g, hipStream_t s);
 hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s);
 hipError_t launch_totals(const TotParams& q, int nparts, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Single-deployment HPA engine (rollout_d1.hip): every BASELINE config 2-4
+// workload. The host digests the world into this block (ccka_abi.cpp,
+// d1_eligible / d1_prepare); the Karpenter launch choice comes from the
+// per-rollout argmin tables built by launch_table.
+// ---------------------------------------------------------------------------
+constexpr int D1_MAX_ZI = 8;   // distinct NodePool zone masks
+constexpr int D1_MAX_WC = 8;   // distinct carbon weights
+constexpr int D1_REC_SAT = 32767;
+
+struct D1Rule {
+  int32_t sel, n, stab_mask, _pad;
+  int32_t type[2], value[2], pmask[2];
+  double factor[2];   // Percent: 1 +/- value/100 (binary64, as the spec writes it)
+  // the same windows as packed int16 lane masks over the 8-entry history
+  // (word r holds entries 2r, 2r+1): stab16 = 0xFFFF per entry in the
+  // stabilisation window, pm16 = 1 per entry inside policy q's period
+  int32_t stab16[4];
+  int32_t pm16[2][4];
+};
+
+// one profile patch of one pool, pre-digested: policy 0 / cas -1 / zi -1 / cm 0 = keep
+struct D1Patch {
+  int32_t policy, cas, zi, cm;  // cas = ceil(consolidate_after_s / 60) steps
+};
+
+struct D1Params {
+  const int32_t* load;       // [T][N]
+  const int32_t* price;      // [R][24][K][Z][2]
+  const double* ci_gpwmin;   // [R][24]
+  const long long* acc;      // [K][3] idle_nw, dyn_nw_per_m, alloc_cpu_m
+  const int2* table;         // [R][24][NZI][3][NW][JT] {price, info}; info -1 = none
+  const int32_t* jtab;       // [R][24][NZI][3] max pods of one new claim
+  // per-scenario overrides (nullable)
+  const uint8_t* region;
+  const int16_t* target;
+  const int16_t* maxr;
+  const int16_t* down_stab;
+  const int16_t* reset_ca;
+  const uint8_t* pswitch;
+  const uint8_t* wci;        // carbon-weight index (NW distinct values)
+  const uint8_t* cap_sel;
+  // results (same buffers as KParams)
+  int64_t* cost;
+  double* energy;
+  double* gco2;
+  int32_t* slo;
+  int64_t* pend_min;
+  int32_t* nmin_spot;
+  int32_t* nmin_od;
+  int32_t* launches;
+  int32_t* deletions;
+  int32_t* peak_nodes;
+  int32_t* final_reps;
+  int32_t* final_nodes;
+  uint32_t* last_choice;
+  uint32_t* hash;
+  ccka_traj_rec* traj;  // nullable
+  int64_t N;
+  int32_t lpw;  // scenarios per wave (<= 64; fewer lanes = less divergence per wave)
+  int32_t T, K, Z, R, NP, maxn, NZI, NW, JT;
+  int32_t start_minute, peak_start, peak_end, pswitch0, delay;
+  int32_t base_nodes, base_type, slo_util, pdb_pct, pdb_member;
+  int32_t replicas0, minr, maxr0, target0, req_cpu, limit, dstab0, reset_ca0, capsel0;
+  double tol_lo, tol_hi;
+  long long base_nw;
+  int32_t ablate;  // profiling-only phase switches (0 in every real run)
+  unsigned long long* stamps;  // diagnostic per-phase cycle totals (nullptr in every real run)
+  D1Rule up, dn;
+  int32_t budget[CCKA_MAX_POOLS];
+  D1Patch patch[CCKA_MAX_POOLS][4];  // base, RESET, OFFPEAK, PEAK
+};
+
+// argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)
+struct TableParams {
+  const int32_t* price;      // [R][24][K][Z][2]
+  const double* ci_gpwh;     // [R][24]
+  const ccka_itype* types;   // [K]
+  const int32_t* order;      // [K] types by pod capacity desc, index asc
+  const int32_t* cap1s;      // [K] pod capacity of order[i]
+  const uint32_t* zmasks;    // [NZI]
+  const double* wc1000;      // [NW] carbon weight * 1000
+  int2* table;
+  int32_t* jtab;
+  int32_t K, Z, R, NZI, NW, JT;
+};
+
+hipError_t launch_table(const TableParams& t, hipStream_t s);
+hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s);
+
 }  // namespace ccka

@@ -471,11 +471,13 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 
   int profile = -1;
   long long cost = 0, pend_min = 0, burn = 0, base_price = 0;
-  double energy = 0.0, gco2 = 0.0, ci_gpwmin = 0.0, ci_gpwh = 0.0;
+  long long energy_nw = 0, e_hour = 0;  // exact nanowatt-minutes (SEMANTICS §3.H)
+  double gco2 = 0.0, ci_gpwmin = 0.0, ci_gpwh = 0.0;
   int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
   uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
   const ccka_itype bt = p.types[base_type];
-  const double base_w = (double)base_nodes * (bt.p_idle_w + bt.p_dyn_w * gw->base_util);
+  const long long base_nw =
+      (long long)base_nodes * (bt.idle_nw + bt.dyn_nw_per_m * (long long)(gw->base_util * (double)bt.alloc_cpu_m));
   const int ps = gw->peak_start_min, pe = gw->peak_end_min;
   const int delay = gw->provision_delay_steps;
 
@@ -515,6 +517,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         __syncthreads();
       }
       if (active) {
+        // carbon of the hour that just ended
+        if (t > 0) gco2 += (double)e_hour * (ci_gpwmin * 1e-9);
+        e_hour = 0;
         ci_gpwmin = s_ci[(rl * 24 + h) * 2 + 0];
         ci_gpwh = s_ci[(rl * 24 + h) * 2 + 1];
         base_price = (long long)base_nodes * tprice(L, rl, base_type, 0, 1);
@@ -1086,36 +1091,34 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         g_wake = wake;
       }
       // ---- H. accounting ----
-      double upp[DMAX];
+      long long upp[DMAX];
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        upp[d] = 0.0;
+        upp[d] = 0;
         if (d >= D) continue;
         const int rd = rpods[d];
         if (rd > 0) {
           long long usage = Lcur[d];
           if (dep[d].limit > 0) usage = min(usage, (long long)rd * dep[d].limit);
-          upp[d] = (double)usage / (double)rd;
+          upp[d] = max(usage, 0LL) / rd;
         }
       }
-      double step_w = base_w;
+      long long e_step = base_nw;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
         if (!(used >> n & 1u) || (p.ablate & 4)) continue;
         const ccka_itype& ty = L.types[ni_type(ninfo[n])];
-        double u = 0.0;
+        long long use = 0;
         if (rdy >> n & 1u) {
-          double xs = 0.0;
 #pragma unroll
-          for (int d = 0; d < DMAX; ++d) if (d < D) xs += (double)npods[n][d] * upp[d];
-          u = xs * ty.inv_alloc_cpu;
-          if (u > 1.0) u = 1.0;
+          for (int d = 0; d < DMAX; ++d) if (d < D) use += (long long)npods[n][d] * upp[d];
+          use = min(use, (long long)ty.alloc_cpu_m);
         }
-        step_w += ty.p_idle_w + ty.p_dyn_w * u;
+        e_step += ty.idle_nw + ty.dyn_nw_per_m * use;
       }
       cost += burn + base_price;
-      energy += step_w;
-      gco2 += step_w * ci_gpwmin;
+      energy_nw += e_step;
+      e_hour += e_step;
       int pending = 0, reps = 0;
       bool viol = false;
 #pragma unroll
@@ -1145,11 +1148,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     }
   }
   if (!active) return;
+  gco2 += (double)e_hour * (ci_gpwmin * 1e-9);
   int reps = 0;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) reps += d < D ? replicas[d] : 0;
   p.cost[i] = cost;
-  p.energy[i] = energy;
+  p.energy[i] = (double)energy_nw * 1e-9;
   p.gco2[i] = gco2;
   p.slo[i] = slo;
   p.pend_min[i] = pend_min;

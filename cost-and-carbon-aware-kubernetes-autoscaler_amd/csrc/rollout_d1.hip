@@ -1,0 +1,875 @@
+// rollout_d1.hip — MI355X (gfx950) rollout engine for single-deployment HPA
+// worlds (BASELINE configs 2-4: one Deployment per cluster scenario).
+//
+// Same semantics as rollout_kernel (docs/SEMANTICS.md), re-planned for the
+// common case so that a quiet step (no scale event) costs a few dozen VALU
+// instructions:
+//   * Karpenter launch choice (SEMANTICS §3.F, the argmin over cost + carbon
+//     weight, spot-first): with one deployment and no pool CPU limits it is a
+//     pure function of (region, hour, zone mask, capacity mask, carbon weight,
+//     pod count). table_kernel evaluates it once per rollout for every key
+//     with wavefront prefix-argmin scans over the catalog sorted by pod
+//     capacity; a launch is then one L2-resident load instead of a
+//     wave-serialised catalog scan per lane.
+//   * HPA utilisation (upstream replica_calculator.go) is a 32-bit integer
+//     division; the 10 % tolerance test is an integer interval on util derived
+//     exactly from the binary64 ratio test. The binary64 proposal arithmetic
+//     runs only on scale events.
+//   * HPA history rings (stabilisation window, rate periods) are packed int16.
+//   * Disruption (Karpenter WhenEmpty / WhenEmptyOrUnderutilized) keeps a
+//     per-slot "consolidatable from step" and is evaluated only when state
+//     changed or a node crossed that threshold; with identical pods the
+//     first-fit re-packing test reduces to a sum of free capacities.
+// Results are bit-identical to the CPU oracle (tests/test_gpu_parity.py).
+//
+// Reference anchors: the NodePool profile patches demo_19_reset_policies.sh:68-75,
+// demo_20_offpeak_configure.sh:59-81, demo_21_peak_configure.sh:56-77; pods
+// demo_30_burst_configure.sh:57-141; PDB demo_10_setup_configure.sh:47-56.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ccka.h"
+#include "kparams.h"
+
+#pragma clang fp contract(off)
+
+namespace ccka {
+
+namespace {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ int capbit1(int c) { return c == 0 ? CCKA_CAP_SPOT : CCKA_CAP_OD; }
+
+// ---------------------------------------------------------------------------
+// argmin tables
+// ---------------------------------------------------------------------------
+struct Best {
+  double s;   // score
+  int k;      // catalog index (tie-break)
+  int info;   // packed k | z<<10 | c<<12 (cap1 added on write)
+  int price;
+};
+
+__device__ __forceinline__ bool better(double s2, int k2, double s, int k) {
+  return s2 < s || (s2 == s && k2 < k);
+}
+
+__device__ __forceinline__ void take_if_better(Best& a, const Best& b) {
+  if (better(b.s, b.k, a.s, a.k)) a = b;
+}
+
+__device__ __forceinline__ Best shfl_up_best(const Best& a, int off) {
+  Best o;
+  o.s = __shfl_up(a.s, off);
+  o.k = __shfl_up(a.k, off);
+  o.info = __shfl_up(a.info, off);
+  o.price = __shfl_up(a.price, off);
+  return o;
+}
+
+__device__ __forceinline__ Best readlane_best(const Best& a, int l) {
+  Best o;
+  const long long b = __double_as_longlong(a.s);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  o.s = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+  o.k = __builtin_amdgcn_readlane(a.k, l);
+  o.info = __builtin_amdgcn_readlane(a.info, l);
+  o.price = __builtin_amdgcn_readlane(a.price, l);
+  return o;
+}
+
+}  // namespace
+
+// One wave per key (region, hour, zone-mask index, capacity mask, carbon
+// weight). Types are visited in pod-capacity-descending order, so the best
+// offering among the first i types is the launch choice for every claim size
+// n in (cap1[order[i+1]], cap1[order[i]]] (SEMANTICS §3.F: candidates hold the
+// claim; spot offerings only, when spot is allowed and any is feasible; the
+// lexicographic minimum of (score, k, z, c)). The per-chunk inclusive prefix
+// argmin is a 6-round wavefront shuffle scan.
+__global__ void __launch_bounds__(256) table_kernel(TableParams q) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t key = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const int64_t nkeys = (int64_t)q.R * 24 * q.NZI * 3 * q.NW;
+  if (key >= nkeys) return;  // wave-uniform
+  int64_t x = key;
+  const int wi = (int)(x % q.NW); x /= q.NW;
+  const int cmi = (int)(x % 3); x /= 3;
+  const int zi = (int)(x % q.NZI); x /= q.NZI;
+  const int rh = (int)x;  // r * 24 + h
+  const uint32_t cm = (uint32_t)cmi + 1u, zm = q.zmasks[zi];
+  const double wc = q.wc1000[wi];
+  const double ci = q.ci_gpwh[rh];
+  const int32_t* tile = q.price + (int64_t)rh * q.K * q.Z * 2;
+  int2* out = q.table + key * q.JT;
+  const double INF = __builtin_inf();
+  Best cs{INF, 0x7fffffff, -1, 0}, ca{INF, 0x7fffffff, -1, 0};
+  int jmax = 0;
+  for (int base = 0; base < q.K; base += WAVE) {
+    const int pos = base + lane;
+    const bool v = pos < q.K;
+    const int k = v ? q.order[pos] : 0;
+    const int c1 = v ? q.cap1s[pos] : 0;
+    const int c1n = pos + 1 < q.K ? q.cap1s[pos + 1] : 0;
+    Best bs{INF, 0x7fffffff, -1, 0}, ba{INF, 0x7fffffff, -1, 0};
+    if (v) {
+      const double carbon = q.types[k].p_ref_w * ci;
+      for (int z = 0; z < q.Z; ++z) {
+        if (!(zm >> z & 1u)) continue;
+        for (int c = 0; c < 2; ++c) {
+          if (!(cm & (uint32_t)capbit1(c))) continue;
+          const int pr = tile[(k * q.Z + z) * 2 + c];
+          if (pr <= 0) continue;
+          const double score = (double)pr + wc * carbon;
+          const int info = k | z << 10 | c << 12;
+          if (score < ba.s) { ba.s = score; ba.k = k; ba.info = info; ba.price = pr; }
+          if (c == 0 && score < bs.s) { bs.s = score; bs.k = k; bs.info = info; bs.price = pr; }
+        }
+      }
+      if (ba.info >= 0) jmax = max(jmax, c1);
+    }
+    // inclusive prefix argmin over the chunk
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+      const Best os = shfl_up_best(bs, off), oa = shfl_up_best(ba, off);
+      if (lane >= off) { take_if_better(bs, os); take_if_better(ba, oa); }
+    }
+    take_if_better(bs, cs);
+    take_if_better(ba, ca);
+    if (v && c1 > c1n) {
+      const Best& w = bs.info >= 0 ? bs : ba;  // spot first when any spot offering holds n
+      const int info = w.info >= 0 ? (w.info | c1 << 16) : -1;
+      const int hi = min(c1, q.JT - 1);
+      for (int n = c1n + 1; n <= hi; ++n) out[n] = make_int2(w.price, info);
+    }
+    cs = readlane_best(bs, WAVE - 1);
+    ca = readlane_best(ba, WAVE - 1);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) jmax = max(jmax, __shfl_xor(jmax, o));
+  if (lane == 0) {
+    q.jtab[key / q.NW] = jmax;  // identical for every carbon weight of the key
+    out[0] = make_int2(0, jmax);
+  }
+}
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// rollout helpers
+// ---------------------------------------------------------------------------
+// Opaque copy of a kernel argument: the value then lives in a register for the
+// whole loop (spilled to a VGPR lane if need be) instead of being re-read from
+// the kernarg segment with an s_load + lgkmcnt wait at each use.
+template <class V>
+__device__ __forceinline__ V opq(V v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+// global-memory pointer made opaque the same way, keeping its address space
+// (a generic pointer would turn every access into a flat_* instruction)
+#define GLOBAL_AS __attribute__((address_space(1)))
+template <class V>
+__device__ __forceinline__ GLOBAL_AS V* opq_ptr(V* v) {
+  uint64_t x = (uint64_t)v;
+  asm volatile("" : "+s"(x));
+  return (GLOBAL_AS V*)x;
+}
+// per-lane variant: the value is redefined by the asm, so no load is pending
+// on it afterwards (the wait for the load happens here, not at its next use)
+__device__ __forceinline__ int opqv(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ D1Rule opq_rule(const D1Rule& r) {
+  D1Rule o;
+  o.sel = opq(r.sel);
+  o.n = opq(r.n);
+  o.stab_mask = opq(r.stab_mask);
+  o._pad = 0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    o.type[q] = opq(r.type[q]);
+    o.value[q] = opq(r.value[q]);
+    o.pmask[q] = opq(r.pmask[q]);
+    o.factor[q] = opq(r.factor[q]);
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    o.stab16[w] = opq(r.stab16[w]);
+    o.pm16[0][w] = opq(r.pm16[0][w]);
+    o.pm16[1][w] = opq(r.pm16[1][w]);
+  }
+  return o;
+}
+
+__device__ __forceinline__ int wmask(int window_s) {
+  int m = 0;
+#pragma unroll
+  for (int k = 0; k < CCKA_HIST; ++k) m |= ((k + 1) * CCKA_STEP_SECONDS < window_s) ? (1 << k) : 0;
+  return m;
+}
+
+// packed int16 history rings: entry k (k steps old, 0 = this step) sits in
+// half k&1 of word k>>1
+__device__ __forceinline__ void ring_push(uint32_t* r, int v) {
+  r[3] = __builtin_amdgcn_alignbit(r[3], r[2], 16);
+  r[2] = __builtin_amdgcn_alignbit(r[2], r[1], 16);
+  r[1] = __builtin_amdgcn_alignbit(r[1], r[0], 16);
+  r[0] = (r[0] << 16) | ((uint32_t)v & 0xFFFFu);
+}
+__device__ __forceinline__ int ring_s(const uint32_t* r, int k) { return (int)(int16_t)(r[k >> 1] >> ((k & 1) * 16)); }
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ short2v as_s2(uint32_t x) { return __builtin_bit_cast(short2v, x); }
+__device__ __forceinline__ uint32_t as_u(short2v x) { return __builtin_bit_cast(uint32_t, x); }
+// (m & a) | (~m & b): v_bfi_b32
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+// convertDesiredReplicasWithBehaviorRate, one direction. The period sums of
+// scale-up / scale-down deltas are packed int16 dot products of the delta
+// ring (entries 1..8 steps old, i.e. the ring BEFORE this step's push) with
+// the policy's period mask.
+__device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, const uint32_t* del) {
+  if (R.sel == CCKA_SELECT_DISABLED) return cur;
+  const bool min_sel = R.sel == CCKA_SELECT_MIN;
+  long long res = (up == min_sel) ? 0x7fffffffLL : -0x80000000LL;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q >= R.n) break;
+    int added = 0, removed = 0;
+    if (R.pmask[q]) {  // wave-uniform
+      const short2v z = {0, 0};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const short2v d = as_s2(del[w]), m = as_s2((uint32_t)R.pm16[q][w]);
+        added = __builtin_amdgcn_sdot2(__builtin_elementwise_max(d, z), m, added, false);
+        removed = __builtin_amdgcn_sdot2(__builtin_elementwise_max(z - d, z), m, removed, false);
+      }
+    }
+    const long long pst = (long long)cur - added + removed;
+    long long pr;
+    if (R.type[q] == CCKA_HPA_PODS) pr = up ? pst + R.value[q] : pst - R.value[q];
+    else if (up) pr = (int)ceil((double)pst * R.factor[q]);
+    else pr = (int)((double)pst * R.factor[q]);
+    res = (up == min_sel) ? min(res, pr) : max(res, pr);
+  }
+  return (int)res;
+}
+
+}  // namespace
+
+// STAMPS: diagnostic build only (never in a real run): per-phase s_memtime
+// cycle totals summed over waves into p.stamps[8].
+#define D1_STAMP(k)                                          \
+  if constexpr (STAMPS) {                                    \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+    st_acc[k] += now_ - st_last;                             \
+    st_last = now_;                                          \
+  }
+
+template <int MAXN, int MAXP, bool STAMPS>
+__global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
+  uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+  // per instance type: {idle_nw lo, idle_nw hi, dyn_nw_per_m, alloc_cpu_m} (one ds_read_b128)
+  extern __shared__ __attribute__((aligned(16))) int4 s_acc[];
+  for (int x = threadIdx.x; x < p.K; x += blockDim.x) {
+    const long long idle = p.acc[x * 3 + 0];
+    s_acc[x] = make_int4((int)(idle & 0xffffffffLL), (int)(idle >> 32), (int)p.acc[x * 3 + 1], (int)p.acc[x * 3 + 2]);
+  }
+  __syncthreads();
+  // lanes-per-wave mapping: wave w owns scenarios [w*lpw, (w+1)*lpw)
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+  const int64_t i = wv * p.lpw + lane;
+  if (lane >= p.lpw || i >= p.N) return;  // no cross-lane operations below
+
+  // ---- per-scenario parameters ----
+  const int r = p.region ? (int)p.region[i] : 0;
+  const int target = p.target ? (int)p.target[i] : p.target0;
+  const int mx = p.maxr ? (int)p.maxr[i] : p.maxr0;
+  const int dnmask = wmask(p.down_stab ? (int)p.down_stab[i] : p.dstab0);
+  const int reset_ca = p.reset_ca ? (int)p.reset_ca[i] : p.reset_ca0;
+  const int pswitch = p.pswitch ? (int)p.pswitch[i] : p.pswitch0;
+  const int wi = p.wci ? (int)p.wci[i] : 0;
+  const uint32_t capsel = p.cap_sel ? (uint32_t)p.cap_sel[i] : (uint32_t)p.capsel0;
+  const int minr = opq(p.minr), req = opq(p.req_cpu), limit = opq(p.limit);
+  // 1-tol <= fl(util/target) <= 1+tol  <=>  ulo <= util <= uhi (fl(u/t) is monotone in u)
+  int ulo = max(0, (int)floor(p.tol_lo * (double)target) - 2);
+  while ((double)ulo / (double)target < p.tol_lo) ++ulo;
+  int uhi = (int)floor(p.tol_hi * (double)target) + 2;
+  while ((double)uhi / (double)target > p.tol_hi) --uhi;
+
+  // ---- kernel arguments used inside the step loop (opaque register copies) ----
+  const int NP = opq(p.NP), NZI = opq(p.NZI), NW = opq(p.NW), JT = opq(p.JT);
+  const int maxn = opq(p.maxn), ablate = opq(p.ablate), pdb_member = opq(p.pdb_member);
+  const int pdb_pct = opq(p.pdb_pct), slo_util = opq(p.slo_util), delay = opq(p.delay);
+  const int base_nodes = opq(p.base_nodes), base_type = opq(p.base_type);
+  const int K = opq(p.K), Z = opq(p.Z), T = opq(p.T);
+  const int ps = opq(p.peak_start), pe = opq(p.peak_end);
+  const long long base_nw = opq(p.base_nw), ls = opq(p.N);
+  const double tol_lo = opq(p.tol_lo), tol_hi = opq(p.tol_hi);
+  const GLOBAL_AS int32_t* const price = opq_ptr(p.price);
+  const GLOBAL_AS double* const ci_gpwmin = opq_ptr(p.ci_gpwmin);
+  const GLOBAL_AS int2* const table = opq_ptr(p.table);
+  const GLOBAL_AS int32_t* const jtab = opq_ptr(p.jtab);
+  GLOBAL_AS int4* const traj = opq_ptr(reinterpret_cast<int4*>(p.traj));
+  const D1Rule rup = opq_rule(p.up), rdn = opq_rule(p.dn);
+  int budget[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) budget[q] = opq(p.budget[q]);
+
+  // ---- NodePools: base spec then RESET (SEMANTICS §1) ----
+  int ppol[MAXP], pcas[MAXP], pzi[MAXP], pJ[MAXP];
+  uint32_t pcm[MAXP], pmask[MAXP];
+#pragma unroll
+  for (int q = 0; q < MAXP; ++q) {
+    ppol[q] = 0; pcas[q] = 0; pzi[q] = -1; pcm[q] = 0; pJ[q] = 0; pmask[q] = 0;
+    if (q < NP) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const D1Patch& x = p.patch[q][s];
+        if (x.policy) ppol[q] = x.policy;
+        if (x.cas >= 0) pcas[q] = s == 1 ? (reset_ca + CCKA_STEP_SECONDS - 1) / CCKA_STEP_SECONDS : x.cas;
+        if (x.zi >= 0) pzi[q] = x.zi;
+        if (x.cm) pcm[q] = (uint32_t)x.cm;
+      }
+    }
+  }
+
+  // consolidateAfter (steps) of a slot's pool: explicit selects on the pool
+  // bits (an indexed pcas[] would be demoted to scratch memory)
+  auto cas_of = [&](uint32_t info) {
+    const int m1 = -(int)(info >> 13 & 1u), m2 = -(int)(info >> 14 & 1u);
+    const int lo = pcas[0] ^ ((pcas[0] ^ pcas[MAXP > 1 ? 1 : 0]) & m1);
+    if constexpr (MAXP <= 2) {
+      return lo;
+    } else {
+      const int hi = pcas[2] ^ ((pcas[2] ^ pcas[3]) & m1);
+      return lo ^ ((lo ^ hi) & m2);
+    }
+  };
+
+  // ---- node slots (register arrays, fully unrolled loops) ----
+  uint32_t sinfo[MAXN];  // type | zone<<10 | cap<<12 | pool<<13
+  int sready[MAXN], slast[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN], selig[MAXN];
+#pragma unroll
+  for (int n = 0; n < MAXN; ++n) {
+    sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0; selig[n] = 0;
+
+  }
+  uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
+  const uint32_t slot_mask = maxn >= 32 ? 0xFFFFFFFFu : ((1u << maxn) - 1u);
+
+  int replicas = p.replicas0, placed = 0, rpods = 0;
+  // HPA history, packed int16, entry k = k+1 steps old at decision time:
+  // recommendations with invalid entries stored as the neutral element of the
+  // max (hdn) and of the min (hup), and scale deltas
+  uint32_t hdn[4], hup[4], hdel[4] = {0, 0, 0, 0};
+  uint32_t dn16[4];  // this scenario's down-stabilisation window as packed lane masks
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    hdn[w] = 0x80008000u;
+    hup[w] = 0x7FFF7FFFu;
+    dn16[w] = ((dnmask >> (2 * w)) & 1 ? 0xFFFFu : 0u) | ((dnmask >> (2 * w + 1)) & 1 ? 0xFFFF0000u : 0u);
+  }
+  int next_ready = 0x7fffffff, nsp = 0, nod = 0;
+  bool dirty = true;
+  int wake = 0;
+  int profile = -1, hour = -1;
+  long long cost = 0, pend_min = 0, burn = 0, base_price = 0;
+  // energy in exact nanowatt-minutes. Cached over the slots (refreshed when a
+  // slot's pods, readiness or existence changed): I = sum of idle draw,
+  // S = sum over ready slots of dyn_nw_per_m * pods, R = max over ready slots
+  // of pods/alloc in binary32: upp*R < 0.9999 proves no node saturates, and
+  // then the step's energy is base + I + upp*S exactly.
+  long long energy_nw = 0, e_hour = 0, Isum = 0, Ssum = 0;
+  float Rmax = 0.f;
+  bool acc_dirty = false;
+  double gco2 = 0.0, ci_min = 0.0;
+  int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
+  uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
+
+  auto refresh_J = [&](int rh) {
+#pragma unroll
+    for (int q = 0; q < MAXP; ++q) {
+      const uint32_t cm = pcm[q] & capsel;
+      pJ[q] = (q < NP && cm && pzi[q] >= 0) ? jtab[((int64_t)rh * NZI + pzi[q]) * 3 + (cm - 1)] : 0;
+    }
+  };
+
+  // load samples software-pipelined one step ahead: a step is long enough to
+  // cover the HBM latency of the next step's coalesced read
+  const int32_t* lp = p.load + i;
+  // Memory pipeline of one step: at its top the previous step's trajectory
+  // record is stored and the next step's load sample is issued; the sample is
+  // taken into a register only at the end of the step, so every wait the
+  // compiler places covers operations that are a whole step old.
+  int Lcur = opqv(lp[0]);
+  int4 rec_prev = make_int4(0, 0, 0, 0);
+  int minute = p.start_minute % 1440;
+
+  for (int t = 0; t < T; ++t, minute = minute == 1439 ? 0 : minute + 1) {
+    if (traj && t > 0) *(int4*)(traj + (int64_t)(t - 1) * ls + i) = rec_prev;
+    const int Lraw = lp[(int64_t)min(t + 1, T - 1) * ls];
+    const int L = Lcur;
+    const int h = minute / 60;
+    const int rh = r * 24 + h;
+    if (h != hour) {  // wave-uniform: this hour's prices and carbon intensity
+      if (hour >= 0) gco2 += (double)e_hour * (ci_min * 1e-9);  // carbon of the hour that ended
+      e_hour = 0;
+      hour = h;
+      const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
+      ci_min = ci_gpwmin[rh];
+      base_price = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
+      burn = 0;
+      // every slot's price in flight at once (unused slots read entry 0)
+      int np[MAXN];
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const uint32_t x = sinfo[n];
+        np[n] = tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
+      }
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        if (used >> n & 1u) {
+          sprice[n] = np[n];
+          burn += np[n];
+        }
+      }
+      refresh_J(rh);
+    }
+    uint32_t flags = 0;
+    int step_last_type = 0xFFFF;
+
+    D1_STAMP(0);
+    // ---- B. readiness ----
+    if (t >= next_ready) {
+      next_ready = 0x7fffffff;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        if ((used & ~rdy) >> n & 1u) {
+          if (sready[n] <= t) { rdy |= 1u << n; rpods += spods[n]; acc_dirty = true; }
+          else next_ready = min(next_ready, sready[n]);
+        }
+      }
+      dirty = true;
+    }
+    // ---- A. profile ----
+    const bool in_win = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
+    const bool peak = pswitch && in_win;
+    const int prof = peak ? CCKA_PROFILE_PEAK : CCKA_PROFILE_OFFPEAK;
+    if (peak) flags |= 1u;
+    if (prof != profile) {
+      profile = prof;
+      dirty = true;
+#pragma unroll
+      for (int q = 0; q < MAXP; ++q) {
+        if (q >= NP) break;
+        const D1Patch& x = p.patch[q][prof + 1];
+        if (x.policy) ppol[q] = x.policy;
+        if (x.cas >= 0) pcas[q] = x.cas;
+        if (x.zi >= 0) pzi[q] = x.zi;
+        if (x.cm) pcm[q] = (uint32_t)x.cm;
+      }
+      // consolidateAfter may have changed: per-slot copies and thresholds
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n)
+        if (used >> n & 1u) selig[n] = max(sready[n], slast[n] + cas_of(sinfo[n]));
+      refresh_J(rh);
+    }
+
+    D1_STAMP(1);
+    // ---- C. HPA ----
+    const int cur = replicas, ready = rpods;
+    int desired = cur, proposal = cur, util = 0;
+    bool ran = false, hpa_path = true, util_valid = false;
+    if (cur == 0 && minr != 0) {
+      hpa_path = false;
+    } else if (cur > mx) {
+      desired = mx;
+    } else if (cur < minr) {
+      desired = minr;
+    } else if (ready > 0) {
+      const long long rcap = (long long)ready * limit;
+      const int usage = (limit > 0 && rcap < (long long)L) ? (int)rcap : L;
+      // int32(usage*100 / (ready*req)): 32-bit unsigned division when it is exact
+      if (usage >= 0 && usage <= 42949672) util = (int)((uint32_t)usage * 100u / (uint32_t)(ready * req));
+      else util = (int)(((long long)usage * 100) / ((long long)ready * req));
+      util_valid = true;
+      ran = true;
+      const bool unready_up = cur > ready && util > target;
+      if (unready_up || util < ulo || util > uhi) {  // scale event: binary64 as the spec writes it
+        const double ratio = (double)util / (double)target;
+        if (cur - ready > 0 && ratio > 1.0) {
+          const int nu = (usage >= 0 && usage <= 42949672)
+                             ? (int)((uint32_t)usage * 100u / (uint32_t)(cur * req))
+                             : (int)(((long long)usage * 100) / ((long long)cur * req));
+          const double nr = (double)nu / (double)target;
+          if ((tol_lo <= nr && nr <= tol_hi) || nr < 1.0) proposal = cur;
+          else proposal = max(cur, (int)ceil(nr * (double)cur));
+        } else if (tol_lo <= ratio && ratio <= tol_hi) {
+          proposal = cur;
+        } else {
+          proposal = (int)ceil(ratio * (double)ready);
+        }
+      }
+    }
+    D1_STAMP(8);
+    if constexpr (STAMPS) st_acc[11] += __ballot(ran && proposal != cur) != 0 ? 1 : 0;
+    if (ran && proposal != cur && !(ablate & 8)) {
+      // stabilisation: packed min / max over the records inside each window
+      int upr = proposal, dnr = proposal;
+      if (rup.stab_mask) {  // wave-uniform
+        short2v a = as_s2(bfi((uint32_t)rup.stab16[0], hup[0], 0x7FFF7FFFu));
+#pragma unroll
+        for (int w = 1; w < 4; ++w)
+          a = __builtin_elementwise_min(a, as_s2(bfi((uint32_t)rup.stab16[w], hup[w], 0x7FFF7FFFu)));
+        upr = min(upr, min((int)a.x, (int)a.y));
+      }
+      {
+        short2v a = as_s2(bfi(dn16[0], hdn[0], 0x80008000u));
+#pragma unroll
+        for (int w = 1; w < 4; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
+        dnr = max(dnr, max((int)a.x, (int)a.y));
+      }
+      int rc = max(cur, upr);
+      rc = min(rc, dnr);
+      int lo = minr, hi = mx;
+      if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
+      else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+      desired = rc < lo ? lo : (rc > hi ? hi : rc);
+    }
+    D1_STAMP(9);
+    // records clamp to int16 (replicas stay in [0, 32767]; min/max commute with clamping)
+    {
+      const int rv = min(max(proposal, -D1_REC_SAT - 1), D1_REC_SAT);
+      ring_push(hdn, ran ? rv : (int)0x8000);
+      ring_push(hup, ran ? rv : 0x7FFF);
+    }
+    ring_push(hdel, (hpa_path && desired != cur) ? desired - cur : 0);
+    if (desired != cur) dirty = true;
+    replicas = desired;
+
+    D1_STAMP(2);
+    // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
+    if (placed > replicas) {
+      int excess = placed - replicas;
+      dirty = true;
+      acc_dirty = true;
+      placed = replicas;
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
+#pragma unroll
+        for (int n = MAXN - 1; n >= 0; --n) {
+          if ((m >> n & 1u) && spods[n] > 0 && excess > 0) {
+            const int k = min(spods[n], excess);
+            spods[n] -= k;
+            excess -= k;
+            slast[n] = t;
+            selig[n] = max(sready[n], t + cas_of(sinfo[n]));
+            if (pass == 1) rpods -= k;
+          }
+        }
+      }
+    }
+    // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
+    int pd = replicas - placed;
+    if (pd > 0) {
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) {
+          if (pd > 0 && (m >> n & 1u)) {
+            const int k = min(scap[n] - spods[n], pd);
+            if (k > 0) {
+              spods[n] += k;
+              pd -= k;
+              placed += k;
+              slast[n] = t;
+              selig[n] = max(sready[n], t + cas_of(sinfo[n]));
+              if (pass == 0) { rpods += k; dirty = true; acc_dirty = true; }
+            }
+          }
+        }
+      }
+    }
+    D1_STAMP(3);
+    // ---- F2. Karpenter provisioning: claims of min(J, pending) pods ----
+    {
+      uint32_t fm = ~used & slot_mask;
+      if (pd > 0 && fm && !(ablate & 2)) {
+        int q = -1, J = 0, zq = 0, cq = 0;
+        uint32_t cm = 0;
+#pragma unroll
+        for (int qq = MAXP - 1; qq >= 0; --qq) {  // first pool in Karpenter order
+          const uint32_t c = pcm[qq] & capsel;
+          if (qq < NP && c && pJ[qq] > 0) { q = qq; J = pJ[qq]; cm = c; zq = pzi[qq]; cq = pcas[qq]; }
+        }
+        if (q >= 0) {
+          const GLOBAL_AS int2* row = table + ((((int64_t)rh * NZI + zq) * 3 + (cm - 1)) * NW + wi) * JT;
+          while (pd > 0 && fm) {
+            const int slot = __ffs((int)fm) - 1;
+            fm &= fm - 1;
+            const int k = min(J, pd);
+            const int2 e = *(const int2*)(row + k);  // never empty: k <= J
+            const int info = e.y, price = e.x;
+            const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
+            const int rs = t + delay;
+            const int el = max(rs, t + cq);
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (n == slot) {
+                sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13);
+                sready[n] = rs;
+                slast[n] = t;
+                spods[n] = k;
+                sprice[n] = price;
+                scap[n] = cap1;
+                selig[n] = el;
+              }
+            }
+            const uint32_t bit = 1u << slot;
+            used |= bit;
+            if (capbit1(bc) & capsel) cmask |= bit;
+#pragma unroll
+            for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
+            placed += k;
+            acc_dirty = true;
+            if (delay == 0) { rdy |= bit; rpods += k; dirty = true; }
+            else next_ready = min(next_ready, rs);
+            if (bc == 0) nsp++; else nod++;
+            burn += price;
+            launches++;
+            last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+            hash = (hash ^ last_choice) * 16777619u;
+            step_last_type = bk;
+            flags |= 2u;
+            pd -= k;
+          }
+        }
+      }
+    }
+
+    D1_STAMP(4);
+    // ---- G. disruption (only when state changed or a node became consolidatable) ----
+    if constexpr (STAMPS) st_acc[10] += __ballot(dirty || t >= wake) != 0 ? 1 : 0;
+    if ((dirty || t >= wake) && !(ablate & 1)) {
+      bool budget_hit = false, any_del = false;
+      // One branch-free pass: consolidatable (ready, idle >= consolidateAfter)
+      // slots, empty slots, the free capacity F of the compatible ready slots
+      // and the next wake-up step.
+      uint32_t elig = 0, empty_m = 0;
+      int F = 0, wk = 0x7fffffff;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        elig |= ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
+        empty_m |= spods[n] == 0 ? (1u << n) : 0u;
+        F += ((rdy & cmask) >> n & 1u) ? scap[n] - spods[n] : 0;
+        wk = ((used >> n & 1u) && selig[n] > t) ? min(wk, selig[n]) : wk;
+      }
+      long long allowed = 0x3fffffffffffffffLL;
+      if (pdb_pct >= 0) {
+        const long long rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
+        allowed = max(rdyp - ((long long)pdb_pct * reps + 99) / 100, 0LL);
+      }
+      // WhenEmptyOrUnderutilized test of every slot (SEMANTICS §3.G): its pods
+      // fit on the other compatible ready slots (F minus its own free space)
+      // and the PDB allows evicting them
+      uint32_t under_m = 0;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const int need = (cmask >> n & 1u) ? scap[n] : spods[n];
+        under_m |= (need <= F && (!pdb_member || (long long)spods[n] <= allowed)) ? (1u << n) : 0u;
+      }
+      uint32_t valid = 0;
+#pragma unroll
+      for (int q = 0; q < MAXP; ++q) {
+        if (q >= NP) break;
+        valid |= elig & pmask[q] & (empty_m | (ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED ? under_m : 0u));
+        if (pmask[q] && (budget[q] * __popc(pmask[q]) + 99) / 100 <= 0) budget_hit = true;
+      }
+      if (valid) {  // exact sequential evaluation (a deletion happens this step)
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q) {
+          if (q >= NP) break;
+          const int npool = __popc(pmask[q]);
+          if (npool == 0) continue;
+          const int qbudget = (budget[q] * npool + 99) / 100;
+          int deleted = 0;
+          while (true) {
+            if (deleted >= qbudget) { budget_hit = true; break; }
+            const uint32_t cand = elig & pmask[q];
+            if (!cand) break;
+            int F = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) if ((rdy & cmask) >> n & 1u) F += scap[n] - spods[n];
+            unsigned long long bkey = ~0ull;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (!(cand >> n & 1u)) continue;
+              const int pods = spods[n];
+              bool ok = pods == 0;
+              if (!ok && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) {
+                const int fo = F - ((cmask >> n & 1u) ? scap[n] - pods : 0);
+                ok = fo >= pods && (!pdb_member || (long long)pods <= allowed);
+              }
+              const unsigned long long key = (unsigned long long)pods << 36 |
+                                             (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
+              if (ok && key < bkey) bkey = key;
+            }
+            if (bkey == ~0ull) break;
+            const int best = (int)(bkey & 15u), bpods = (int)(bkey >> 36);
+            // move the candidate's pods first-fit onto the other compatible ready nodes
+            int need = bpods;
+            const uint32_t recv = rdy & cmask & ~(1u << best);
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (need > 0 && (recv >> n & 1u)) {
+                const int k = min(scap[n] - spods[n], need);
+                if (k > 0) {
+                  spods[n] += k;
+                  need -= k;
+                  slast[n] = t;
+                  selig[n] = max(sready[n], t + cas_of(sinfo[n]));
+                }
+              }
+            }
+            // delete the node (its pods moved between ready nodes: running counts unchanged)
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (n == best) {
+                if ((sinfo[n] >> 12 & 1u) == 0) nsp--; else nod--;
+                burn -= sprice[n];
+                sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
+                selig[n] = 0;
+              }
+            }
+            const uint32_t nb = ~(1u << best);
+            used &= nb; rdy &= nb; cmask &= nb; pmask[q] &= nb;
+            if (pdb_member) allowed -= bpods;
+            deleted++;
+            deletions++;
+            any_del = true;
+            acc_dirty = true;
+            flags |= 4u;
+            elig = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) elig |= ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
+          }
+        }
+      }
+      dirty = budget_hit || any_del;
+      if (any_del) {  // slots changed: next step at which a node becomes consolidatable
+        wk = 0x7fffffff;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) if ((used >> n & 1u) && selig[n] > t) wk = min(wk, selig[n]);
+      }
+      wake = wk;
+    }
+
+    D1_STAMP(5);
+    // ---- H. accounting ----
+    if (acc_dirty) {  // branch-free refresh of the cached sums
+      acc_dirty = false;
+      Isum = 0;
+      Ssum = 0;
+      Rmax = 0.f;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const int4 a = s_acc[sinfo[n] & 1023u];
+        const int pr = (rdy >> n & 1u) ? spods[n] : 0;
+        const long long idle = ((long long)a.y << 32) | (unsigned)a.x;
+        Isum += (used >> n & 1u) ? idle : 0;
+        Ssum += (long long)((unsigned long long)(unsigned)a.z * (unsigned)pr);
+        Rmax = fmaxf(Rmax, (float)pr * __builtin_amdgcn_rcpf((float)a.w));
+      }
+    }
+    int upp = 0;
+    if (rpods > 0) {
+      const long long rcap = (long long)rpods * limit;
+      const int usage = (limit > 0 && rcap < (long long)L) ? (int)rcap : L;
+      upp = (int)((uint32_t)max(usage, 0) / (uint32_t)rpods);
+    }
+    long long e_step;
+    if ((float)upp * Rmax < 0.9999f && !(ablate & 4)) {
+      e_step = base_nw + Isum + (long long)upp * Ssum;
+    } else {  // a node saturates (use clamped at its allocatable CPU)
+      e_step = base_nw;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        if (!(used >> n & 1u)) continue;
+        const int4 a = s_acc[sinfo[n] & 1023u];
+        long long use = 0;
+        if (rdy >> n & 1u) use = min((long long)spods[n] * upp, (long long)a.w);
+        e_step += (((long long)a.y << 32) | (unsigned)a.x) + (long long)(unsigned)a.z * use;
+      }
+    }
+    cost += burn + base_price;
+    energy_nw += e_step;
+    e_hour += e_step;
+    const int pending = replicas - rpods;
+    if (pending > 0 || (util_valid && util > slo_util)) { slo++; flags |= 8u; }
+    pend_min += pending;
+    nmin_spot += nsp;
+    nmin_od += nod;
+    peak_nodes = max(peak_nodes, nsp + nod);
+    D1_STAMP(6);
+    rec_prev = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16,
+                         (step_last_type & 0xFFFF) | (int)(flags << 16));
+    Lcur = opqv(Lraw);
+  }
+  if (traj) *(int4*)(traj + (int64_t)(T - 1) * ls + i) = rec_prev;
+  D1_STAMP(7);
+  if constexpr (STAMPS) {
+    if (lane == (__ffsll((long long)__ballot(1)) - 1))
+      for (int k = 0; k < 12; ++k) atomicAdd(&p.stamps[k], (unsigned long long)st_acc[k]);
+  }
+  gco2 += (double)e_hour * (ci_min * 1e-9);
+  p.cost[i] = cost;
+  p.energy[i] = (double)energy_nw * 1e-9;
+  p.gco2[i] = gco2;
+  p.slo[i] = slo;
+  p.pend_min[i] = pend_min;
+  p.nmin_spot[i] = nmin_spot;
+  p.nmin_od[i] = nmin_od;
+  p.launches[i] = launches;
+  p.deletions[i] = deletions;
+  p.peak_nodes[i] = peak_nodes;
+  p.final_reps[i] = replicas;
+  p.final_nodes[i] = __popc(used);
+  p.last_choice[i] = last_choice;
+  p.hash[i] = hash;
+}
+
+hipError_t launch_table(const TableParams& t, hipStream_t s) {
+  const int64_t nkeys = (int64_t)t.R * 24 * t.NZI * 3 * t.NW;
+  const unsigned grid = (unsigned)((nkeys * WAVE + 255) / 256);
+  hipLaunchKernelGGL(table_kernel, dim3(grid), dim3(256), 0, s, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
+  const int B = 256;
+  const int64_t waves = (p.N + p.lpw - 1) / p.lpw;
+  const unsigned grid = (unsigned)((waves + B / WAVE - 1) / (B / WAVE));
+  const size_t lds = (size_t)p.K * sizeof(int4);
+  if (p.stamps)
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true>), dim3(grid), dim3(B), lds, s, p);
+  else if (p.maxn <= 8 && p.NP <= 2)
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false>), dim3(grid), dim3(B), lds, s, p);
+  else if (p.maxn <= 8)
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false>), dim3(grid), dim3(B), lds, s, p);
+  else if (p.NP <= 2)
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false>), dim3(grid), dim3(B), lds, s, p);
+  else
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false>), dim3(grid), dim3(B), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace ccka

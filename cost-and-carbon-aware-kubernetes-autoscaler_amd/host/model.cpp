@@ -94,10 +94,10 @@ Tables builtin_tables(const std::string& which, double ci, uint64_t seed) {
       const int64_t mem_mi = (int64_t)v * fams[f].gib * 1024;
       t.alloc_mem_mi = (int32_t)((mem_mi * 925) / 1000 - (11 * sz.pods + 255) - 100);
       t.max_pods = sz.pods;
-      t.p_idle_w = (double)v * 0.74 * 1.135;
-      t.p_dyn_w = (double)v * (3.5 - 0.74) * 1.135;
-      t.p_ref_w = t.p_idle_w + 0.5 * t.p_dyn_w;
-      t.inv_alloc_cpu = 1.0 / (double)t.alloc_cpu_m;
+      const double p_idle = (double)v * 0.74 * 1.135, p_dyn = (double)v * (3.5 - 0.74) * 1.135;
+      t.idle_nw = std::llround(p_idle * 1e9);
+      t.dyn_nw_per_m = std::llround(p_dyn * 1e9 / (double)t.alloc_cpu_m);
+      t.p_ref_w = p_idle + 0.5 * p_dyn;
       T.types.push_back(t);
       od.push_back(fams[f].uph * v / 2);
     }

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CCKA_ABI_VERSION 1
+#define CCKA_ABI_VERSION 2
 
 #define CCKA_STEP_SECONDS 60
 #define CCKA_MAX_TYPES 1024
@@ -64,17 +64,18 @@ enum { CCKA_SELECT_MAX = 0, CCKA_SELECT_MIN = 1, CCKA_SELECT_DISABLED = 2 };
 enum { CCKA_HPA_PODS = 1, CCKA_HPA_PERCENT = 2 };
 
 /* One EC2 instance type of the catalog (the ~800-entry catalog Karpenter's AWS
- * provider discovers at runtime, 05_karpenter.sh:64-75). Doubles are
- * precomputed by the host from the power model. 48 bytes. */
+ * provider discovers at runtime, 05_karpenter.sh:64-75). The power model
+ *  is precomputed by the host: energy is accounted in exact
+ * integer nanowatt-minutes (docs/SEMANTICS.md §3.H). 48 bytes. */
 typedef struct ccka_itype {
   int32_t vcpu;
-  int32_t alloc_cpu_m;    /* allocatable millicores (after kube-reserved)   */
-  int32_t alloc_mem_mi;   /* allocatable MiB                                */
+  int32_t alloc_cpu_m;    /* allocatable millicores (after kube-reserved)      */
+  int32_t alloc_mem_mi;   /* allocatable MiB                                   */
   int32_t max_pods;
-  double p_idle_w;        /* vcpu*Wmin*PUE                                  */
-  double p_dyn_w;         /* vcpu*(Wmax-Wmin)*PUE                           */
-  double p_ref_w;         /* p_idle_w + 0.5*p_dyn_w (launch-score power)    */
-  double inv_alloc_cpu;   /* 1.0/alloc_cpu_m                                */
+  int64_t idle_nw;        /* llround(vcpu*Wmin*PUE * 1e9)                      */
+  int64_t dyn_nw_per_m;   /* llround(vcpu*(Wmax-Wmin)*PUE * 1e9 / alloc_cpu_m) */
+  double p_ref_w;         /* p_idle + 0.5*p_dyn in W (launch-score power)      */
+  double _reserved;
 } ccka_itype;
 
 /* A NodePool patch profile (merge semantics: 0 / -1 = keep). */

@@ -318,7 +318,8 @@ typedef struct {
   o_node nodes[CCKA_MAX_NODES];
   int profile;
   int64_t cost, pend_min;
-  double energy, gco2;
+  int64_t energy_nw, e_hour; /* nanowatt-minutes: total, current clock hour */
+  double gco2;
   int slo, nmin_spot, nmin_od, launches, deletions, peak_nodes;
   uint32_t last_choice, hash;
 } o_state;
@@ -362,12 +363,20 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
   st.hash = 2166136261u;
   st.last_choice = 0xFFFFFFFFu;
   const ccka_itype* bt = &w->types[w->base_type];
-  const double base_w = (double)w->base_nodes * (bt->p_idle_w + bt->p_dyn_w * w->base_util);
+  const int64_t base_nw = (int64_t)w->base_nodes *
+                          (bt->idle_nw + bt->dyn_nw_per_m * (int64_t)(w->base_util * (double)bt->alloc_cpu_m));
+  int prev_h = -1;
   const int ps = w->peak_start_min, pe = w->peak_end_min;
 
   for (int t = 0; t < w->n_steps; ++t) {
     const int minute = (w->start_minute + t) % 1440;
     const int h = minute / 60;
+    /* carbon is charged per clock hour (SEMANTICS §3.H) */
+    if (prev_h >= 0 && h != prev_h) {
+      st.gco2 += (double)st.e_hour * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
+      st.e_hour = 0;
+    }
+    prev_h = h;
     uint16_t flags = 0;
     uint16_t step_last_type = 0xFFFF;
     /* ---- A. profile ---- */
@@ -673,34 +682,37 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     {
       int64_t cost = (int64_t)w->base_nodes * o_price(e, r, h, w->base_type, 0, 1);
       int ready_d[CCKA_MAX_DEPLOY];
-      double upp[CCKA_MAX_DEPLOY];
+      int64_t upp[CCKA_MAX_DEPLOY];
       for (int d = 0; d < D; ++d) {
         int rd = 0;
         for (int n = 0; n < NN; ++n)
           if (st.nodes[n].used && st.nodes[n].ready_step <= t) rd += st.nodes[n].pods[d];
         ready_d[d] = rd;
-        upp[d] = rd > 0 ? (double)o_usage(Lt[d], rd, w->deploy[d].limit_cpu_m) / (double)rd : 0.0;
+        upp[d] = 0;
+        if (rd > 0) {
+          int64_t u = o_usage(Lt[d], rd, w->deploy[d].limit_cpu_m);
+          if (u < 0) u = 0;
+          upp[d] = u / rd;
+        }
       }
-      double step_w = base_w;
+      int64_t e_step = base_nw;
       int nsp = 0, nod = 0;
       for (int n = 0; n < NN; ++n) {
         const o_node* nd = &st.nodes[n];
         if (!nd->used) continue;
         const ccka_itype* ty = &w->types[nd->type];
         cost += o_price(e, r, h, nd->type, nd->zone, nd->cap);
-        double u = 0.0;
+        int64_t use = 0;
         if (nd->ready_step <= t) {
-          double x = 0.0;
-          for (int d = 0; d < D; ++d) x += (double)nd->pods[d] * upp[d];
-          u = x * ty->inv_alloc_cpu;
-          if (u > 1.0) u = 1.0;
+          for (int d = 0; d < D; ++d) use += (int64_t)nd->pods[d] * upp[d];
+          if (use > ty->alloc_cpu_m) use = ty->alloc_cpu_m;
         }
-        step_w += ty->p_idle_w + ty->p_dyn_w * u;
+        e_step += ty->idle_nw + ty->dyn_nw_per_m * use;
         if (nd->cap == 0) nsp++; else nod++;
       }
       st.cost += cost;
-      st.energy += step_w;
-      st.gco2 += step_w * w->ci_gpwmin[r * 24 + h];
+      st.energy_nw += e_step;
+      st.e_hour += e_step;
       int pending = 0, viol = 0, reps = 0;
       for (int d = 0; d < D; ++d) {
         pending += st.dep[d].replicas - ready_d[d];
@@ -726,11 +738,12 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       }
     }
   }
+  if (prev_h >= 0) st.gco2 += (double)st.e_hour * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
   int reps = 0, nodes = 0;
   for (int d = 0; d < D; ++d) reps += st.dep[d].replicas;
   for (int n = 0; n < NN; ++n) nodes += st.nodes[n].used;
   if (out->cost_uphmin) out->cost_uphmin[i] = st.cost;
-  if (out->energy_wmin) out->energy_wmin[i] = st.energy;
+  if (out->energy_wmin) out->energy_wmin[i] = (double)st.energy_nw * 1e-9;
   if (out->gco2) out->gco2[i] = st.gco2;
   if (out->slo_minutes) out->slo_minutes[i] = st.slo;
   if (out->pending_pod_minutes) out->pending_pod_minutes[i] = st.pend_min;

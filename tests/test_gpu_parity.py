@@ -151,3 +151,98 @@ def test_deterministic_rerun(engine):
     for f in r1:
         assert np.array_equal(r1[f], r2[f]), f
     assert np.array_equal(t1, t2)
+
+
+# ---------------------------------------------------------------------------
+# single-deployment engine (rollout_d1.hip) vs general kernel vs oracle
+# ---------------------------------------------------------------------------
+def test_engine_selection(engine):
+    spec = configs.config2_world(n_steps=60)
+    sc = configs.hpa_scenarios(300)
+    load = po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n)
+    run_engine(engine, spec, sc, load=load)
+    assert engine.last_engine()[0] == 2  # config 2 runs on the single-deployment kernel
+    for p in spec.pools:
+        p.limit_cpu_m = 8000  # pool limits: launch choice depends on pool usage
+    run_engine(engine, spec, sc, load=load)
+    assert engine.last_engine()[0] == 1
+
+
+def _sweep_scenarios(n, first_id=0):
+    """config-4-style per-scenario policy parameters (targets, down-stabilisation
+    windows, consolidateAfter, peak switch, carbon weights, capacity types)."""
+    ids = np.arange(first_id, first_id + n, dtype=np.uint64)
+    sc = configs.hpa_scenarios(n, first_id, 1, None, (0.0, 0.5, 1.0, 2.0))
+    sc.target_util_pct = (40 + 3 * (configs.splitmix32(ids, 11) % 16)).astype(np.int16)
+    sc.down_stab_s = (60 * (configs.splitmix32(ids, 12) % 8)).astype(np.int16)
+    sc.reset_ca_s = np.array([30, 60, 120, 300], np.int16)[configs.splitmix32(ids, 13) % 4]
+    sc.peak_switch = (configs.splitmix32(ids, 14) % 2).astype(np.uint8)
+    sc.cap_sel = (1 + configs.splitmix32(ids, 15) % 3).astype(np.uint8)
+    return sc
+
+
+def test_d1_policy_sweep_parity(engine):
+    spec = configs.config2_world(n_steps=720)
+    n = 2500
+    sc = _sweep_scenarios(n, 99)
+    load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=99)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert rc["deletions"].sum() > 0 and len(set(rc["last_choice"] & 0xFFF)) > 3
+    compare(rg, rc, tg, tc)
+
+
+@pytest.mark.parametrize("variant", ["slots16", "delay0", "tol0", "big_load", "neg_load",
+                                     "no_limit_cpu", "behavior", "budget50", "one_pool"])
+def test_d1_edge_cases(engine, variant):
+    spec = configs.config2_world(n_steps=480)
+    n = 700
+    sc = configs.hpa_scenarios(n, 5)
+    load = po.gen_load(configs.trace_gen(8), spec.n_steps, 1, n, first_id=5)
+    if variant == "slots16":
+        spec.max_nodes = 16
+        load = load * 6
+    elif variant == "delay0":
+        spec.provision_delay_steps = 0
+    elif variant == "tol0":
+        spec.deploys = [deployment(abi.SCALER_HPA, tol=0.0)]
+    elif variant == "big_load":  # usage*100 beyond 32 bits: int64 utilisation path
+        load[::7] = np.int32(2_000_000_000)
+    elif variant == "neg_load":
+        load[::5] = -load[::5]
+    elif variant == "no_limit_cpu":
+        spec.deploys = [deployment(abi.SCALER_HPA, limit_cpu=0)]
+    elif variant == "behavior":
+        from ccka.world import hpa_rules
+        up = hpa_rules(abi.SELECT_MIN, [(abi.HPA_PODS, 2, 120), (abi.HPA_PERCENT, 50, 240)], 120)
+        dn = hpa_rules(abi.SELECT_MAX, [(abi.HPA_PODS, 1, 180), (abi.HPA_PERCENT, 30, 60)], 240)
+        spec.deploys = [deployment(abi.SCALER_HPA, up=up, down=dn, min_r=2, max_r=60)]
+    elif variant == "budget50":
+        spec.max_nodes = 16
+        for p in spec.pools:
+            p.budget_pct = 50
+        load = load * 5
+    elif variant == "one_pool":
+        spec.pools = spec.pools[1:]
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2, variant
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
+
+
+def test_d1_matches_general_kernel(engine):
+    spec = configs.config3_world(n_steps=360)
+    n = 1500
+    sc = configs.hpa_scenarios(n, 0, 8, 190, configs.CONFIG3_CARBON)
+    load = po.gen_load(configs.trace_gen(), spec.n_steps, 1, n)
+    r2, t2 = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    engine.set_engine(1)
+    try:
+        engine.rollout(trajectory=True)
+        assert engine.last_engine()[0] == 1
+        r1, t1 = engine.results(), engine.trajectory()
+    finally:
+        engine.set_engine(0)
+    compare(r2, r1, t2, t1)
