@@ -87,7 +87,7 @@ struct ccka_ctx {
   int JT = 0, NW = 0;
   int engine_mode = 0;       // 0 auto, 1 general kernel only (ccka_debug_engine)
   unsigned long long* d_stamps = nullptr;
-  int lpw = 64;              // scenarios per wave of the single-deployment kernel
+  int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
   int last_engine = 0;       // 1 general, 2 single-deployment
 };
 
@@ -683,7 +683,15 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     p.last_choice = k.last_choice; p.hash = k.hash; p.traj = k.traj;
     p.N = c->N;
     p.NW = c->NW;
-    p.lpw = c->lpw;
+    // scenarios per wave: a wave's cost is the union of its lanes' event paths,
+    // so when the batch is smaller than one full round of resident waves (two
+    // per SIMD at this kernel's register budget) spread it over all of them
+    if (c->lpw > 0) {
+      p.lpw = c->lpw;
+    } else {
+      const int64_t slots = 2LL * 4 * c->cus;  // resident waves: 2 per SIMD, 4 SIMDs per CU
+      p.lpw = (int32_t)std::min<int64_t>(64, std::max<int64_t>(32, (c->N + slots - 1) / slots));
+    }
     p.ablate = k.ablate;
     p.stamps = nullptr;
     if (k.ablate & 16) {  // diagnostic phase stamps (single-deployment engine, 8 slots, 2 pools)
@@ -849,9 +857,9 @@ int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
   return CCKA_OK;
 }
 
-// Internal: scenarios per wave of the single-deployment kernel (1..64).
+// Internal: scenarios per wave of the single-deployment kernel (1..64; 0 = automatic).
 int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
-  if (!c || lpw < 1 || lpw > 64) return CCKA_EINVAL;
+  if (!c || lpw < 0 || lpw > 64) return CCKA_EINVAL;
   c->lpw = lpw;
   return CCKA_OK;
 }

@@ -356,9 +356,12 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
   // ---- node slots (register arrays, fully unrolled loops) ----
   uint32_t sinfo[MAXN];  // type | zone<<10 | cap<<12 | pool<<13
   int sready[MAXN], slast[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN], selig[MAXN];
+  uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
+  float sinvf[MAXN];    // 1/alloc (saturation pre-test only; the energy itself is exact)
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
     sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0; selig[n] = 0;
+    sdyn[n] = 0; sinvf[n] = 0.f;
 
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
@@ -622,6 +625,7 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
             const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
             const int rs = t + delay;
             const int el = max(rs, t + cq);
+            const int4 ac = s_acc[bk];
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
               if (n == slot) {
@@ -632,6 +636,8 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
                 sprice[n] = price;
                 scap[n] = cap1;
                 selig[n] = el;
+                sdyn[n] = (uint32_t)ac.z;
+                sinvf[n] = __builtin_amdgcn_rcpf((float)ac.w);
               }
             }
             const uint32_t bit = 1u << slot;
@@ -641,6 +647,7 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
             for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
             placed += k;
             acc_dirty = true;
+            Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
             if (delay == 0) { rdy |= bit; rpods += k; dirty = true; }
             else next_ready = min(next_ready, rs);
             if (bc == 0) nsp++; else nod++;
@@ -664,15 +671,28 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
       // One branch-free pass: consolidatable (ready, idle >= consolidateAfter)
       // slots, empty slots, the free capacity F of the compatible ready slots
       // and the next wake-up step.
-      uint32_t elig = 0, empty_m = 0;
-      int F = 0, wk = 0x7fffffff;
+      uint32_t eb[MAXN], mb[MAXN];
+      int fv[MAXN], wv[MAXN];
 #pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        elig |= ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
-        empty_m |= spods[n] == 0 ? (1u << n) : 0u;
-        F += ((rdy & cmask) >> n & 1u) ? scap[n] - spods[n] : 0;
-        wk = ((used >> n & 1u) && selig[n] > t) ? min(wk, selig[n]) : wk;
+      for (int n = 0; n < MAXN; ++n) {  // independent per-slot terms, then pairwise trees
+        eb[n] = ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
+        mb[n] = spods[n] == 0 ? (1u << n) : 0u;
+        fv[n] = ((rdy & cmask) >> n & 1u) ? scap[n] - spods[n] : 0;
+        wv[n] = ((used >> n & 1u) && selig[n] > t) ? selig[n] : 0x7fffffff;
       }
+#pragma unroll
+      for (int w = MAXN / 2; w > 0; w >>= 1)
+#pragma unroll
+        for (int n = 0; n < w; ++n) {
+          eb[n] |= eb[n + w];
+          mb[n] |= mb[n + w];
+          fv[n] += fv[n + w];
+          wv[n] = min(wv[n], wv[n + w]);
+        }
+      uint32_t elig = eb[0];
+      const uint32_t empty_m = mb[0];
+      const int F = fv[0];
+      int wk = wv[0];
       long long allowed = 0x3fffffffffffffffLL;
       if (pdb_pct >= 0) {
         const long long rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
@@ -681,12 +701,18 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
       // WhenEmptyOrUnderutilized test of every slot (SEMANTICS §3.G): its pods
       // fit on the other compatible ready slots (F minus its own free space)
       // and the PDB allows evicting them
-      uint32_t under_m = 0;
+      uint32_t ub[MAXN];
+      const int allowed32 = (int)min(allowed, 0x7fffffffLL);
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
         const int need = (cmask >> n & 1u) ? scap[n] : spods[n];
-        under_m |= (need <= F && (!pdb_member || (long long)spods[n] <= allowed)) ? (1u << n) : 0u;
+        ub[n] = (need <= F && (!pdb_member || spods[n] <= allowed32)) ? (1u << n) : 0u;
       }
+#pragma unroll
+      for (int w = MAXN / 2; w > 0; w >>= 1)
+#pragma unroll
+        for (int n = 0; n < w; ++n) ub[n] |= ub[n + w];
+      const uint32_t under_m = ub[0];
       uint32_t valid = 0;
 #pragma unroll
       for (int q = 0; q < MAXP; ++q) {
@@ -746,6 +772,10 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
               if (n == best) {
                 if ((sinfo[n] >> 12 & 1u) == 0) nsp--; else nod--;
                 burn -= sprice[n];
+                const int4 ac = s_acc[sinfo[n] & 1023u];
+                Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
+                sdyn[n] = 0;
+                sinvf[n] = 0.f;
                 sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
                 selig[n] = 0;
               }
@@ -775,20 +805,22 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
 
     D1_STAMP(5);
     // ---- H. accounting ----
-    if (acc_dirty) {  // branch-free refresh of the cached sums
+    if (acc_dirty) {  // branch-free refresh of the cached sums (I is kept incrementally)
       acc_dirty = false;
-      Isum = 0;
-      Ssum = 0;
-      Rmax = 0.f;
+      long long sv[MAXN];
+      float rv[MAXN];
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        const int4 a = s_acc[sinfo[n] & 1023u];
         const int pr = (rdy >> n & 1u) ? spods[n] : 0;
-        const long long idle = ((long long)a.y << 32) | (unsigned)a.x;
-        Isum += (used >> n & 1u) ? idle : 0;
-        Ssum += (long long)((unsigned long long)(unsigned)a.z * (unsigned)pr);
-        Rmax = fmaxf(Rmax, (float)pr * __builtin_amdgcn_rcpf((float)a.w));
+        sv[n] = (long long)((unsigned long long)sdyn[n] * (unsigned)pr);
+        rv[n] = (float)pr * sinvf[n];
       }
+#pragma unroll
+      for (int w = MAXN / 2; w > 0; w >>= 1)  // pairwise trees: short dependency chains
+#pragma unroll
+        for (int n = 0; n < w; ++n) { sv[n] += sv[n + w]; rv[n] = fmaxf(rv[n], rv[n + w]); }
+      Ssum = sv[0];
+      Rmax = rv[0];
     }
     int upp = 0;
     if (rpods > 0) {
@@ -800,14 +832,13 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
     if ((float)upp * Rmax < 0.9999f && !(ablate & 4)) {
       e_step = base_nw + Isum + (long long)upp * Ssum;
     } else {  // a node saturates (use clamped at its allocatable CPU)
-      e_step = base_nw;
+      e_step = base_nw + Isum;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        if (!(used >> n & 1u)) continue;
+        if (!(rdy >> n & 1u)) continue;
         const int4 a = s_acc[sinfo[n] & 1023u];
-        long long use = 0;
-        if (rdy >> n & 1u) use = min((long long)spods[n] * upp, (long long)a.w);
-        e_step += (((long long)a.y << 32) | (unsigned)a.x) + (long long)(unsigned)a.z * use;
+        const long long use = min((long long)spods[n] * upp, (long long)a.w);
+        e_step += (long long)(unsigned)a.z * use;
       }
     }
     cost += burn + base_price;
