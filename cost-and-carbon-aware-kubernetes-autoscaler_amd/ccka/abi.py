@@ -81,7 +81,7 @@ class World(C.Structure):
 
 
 class Scenarios(C.Structure):
-    _fields_ = [("n", C.c_int64), ("first_id", C.c_int64),
+    _fields_ = [("n", C.c_int64), ("first_id", C.c_int64), ("n_traces", C.c_int64),
                 ("region", C.POINTER(C.c_uint8)), ("target_util_pct", C.POINTER(C.c_int16)),
                 ("max_replicas", C.POINTER(C.c_int16)), ("down_stab_s", C.POINTER(C.c_int16)),
                 ("reset_ca_s", C.POINTER(C.c_int16)), ("peak_switch", C.POINTER(C.c_uint8)),
@@ -115,6 +115,11 @@ class Totals(C.Structure):
                 ("energy_wmin", C.c_double), ("gco2", C.c_double)]
 
 
+class GridStats(C.Structure):
+    _fields_ = [("grid", C.c_int64), ("scenarios", C.c_int64), ("cost_uphmin", C.c_int64),
+                ("slo_minutes", C.c_int64), ("gco2", C.c_double), ("energy_wmin", C.c_double)]
+
+
 class TraceGen(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("base_lo", C.c_int32), ("base_hi", C.c_int32),
                 ("amp_lo_pm", C.c_int32), ("amp_hi_pm", C.c_int32), ("noise_pm", C.c_int32),
@@ -122,7 +127,8 @@ class TraceGen(C.Structure):
                 ("burst_len", C.c_int32)]
 
 
-STRUCT_ORDER = [ItType, Pool, Deployment, World, Scenarios, Results, TrajRec, Totals, TraceGen]
+STRUCT_ORDER = [ItType, Pool, Deployment, World, Scenarios, Results, TrajRec, Totals, TraceGen,
+                GridStats]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ENGINE_LIB = os.path.join(os.path.dirname(PKG_DIR), "csrc", "build", "libccka.so")
@@ -194,7 +200,9 @@ EXPORTED = [
     "ccka_set_world", "ccka_set_scenarios", "ccka_set_load", "ccka_gen_load", "ccka_get_load",
     "ccka_rollout", "ccka_rollout_async", "ccka_sync", "ccka_last_kernel_ms", "ccka_get_results",
     "ccka_get_trajectory", "ccka_get_totals", "ccka_comm_unique_id", "ccka_comm_init",
-    "ccka_allreduce_totals", "ccka_device_info",
+    "ccka_allreduce_totals", "ccka_device_info", "ccka_get_grid_stats", "ccka_pareto_frontier",
+    "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
+    "ccka_mlp_forward_async", "ccka_mlp_get_actions",
 ]
 
 

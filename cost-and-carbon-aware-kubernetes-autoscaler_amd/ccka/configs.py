@@ -87,3 +87,69 @@ def config1_world() -> WorldSpec:
     return WorldSpec(catalog=cat, ci=carbon_intensity(1, SEED), price=price_tiles(cat, 1, 3, SEED),
                      pools=reference_pools(), deploys=burst_deployments(12, 5), n_steps=1440,
                      max_nodes=16)
+
+
+# ---------------------------------------------------------------------------
+# config 4: policy sweep, 4096 grids x 1024 shared load traces
+# ---------------------------------------------------------------------------
+CONFIG4_GRIDS = 4096
+CONFIG4_TRACES = 1024
+CONFIG4_CA = (30, 60, 120, 300)
+CONFIG4_CARBON = (0.0, 0.5, 1.0, 2.0)
+
+
+def config4_grid_params(grids: np.ndarray) -> dict:
+    """16 target utilisations (40..85 %) x 8 down-stabilisation windows (0..420 s)
+    x 4 consolidateAfter x 4 carbon weights x peak switch on/off = 4096 grids."""
+    g = np.asarray(grids, np.int64)
+    return {
+        "target_util_pct": (40 + 3 * (g % 16)).astype(np.int16),
+        "down_stab_s": (60 * ((g // 16) % 8)).astype(np.int16),
+        "reset_ca_s": np.asarray(CONFIG4_CA, np.int16)[(g // 128) % 4],
+        "carbon_weight": np.asarray(CONFIG4_CARBON, np.float64)[(g // 512) % 4],
+        "peak_switch": (1 - (g // 2048) % 2).astype(np.uint8),
+    }
+
+
+def config4_scenarios(grid_lo: int, n_grids: int, n_traces: int = CONFIG4_TRACES) -> ScenarioSet:
+    """Grids [grid_lo, grid_lo + n_grids) x n_traces shared traces; scenario
+    global id = grid * n_traces + trace (shard by grid: SURVEY.md 8(e))."""
+    first = grid_lo * n_traces
+    ids = np.arange(first, first + n_grids * n_traces, dtype=np.int64)
+    prm = config4_grid_params(ids // n_traces)
+    trace = ids % n_traces
+    cap = np.where(trace % 2 == 0, abi.CAP_SPOT, abi.CAP_OD).astype(np.uint8)
+    return ScenarioSet(len(ids), first, n_traces, cap_sel=cap, **prm)
+
+
+def config4_trace_gen() -> abi.TraceGen:
+    return trace_gen(SEED + 1)
+
+
+# ---------------------------------------------------------------------------
+# config 5: learned MLP control policy 64 -> 256 -> 256 -> 8 (bf16)
+# ---------------------------------------------------------------------------
+MLP_SHAPE = (64, 256, 256, 8)
+
+
+def mlp_weights(seed: int = 11):
+    """Xavier-uniform weights (fp32), zero-mean small biases; row-major [in][out]."""
+    rng = np.random.default_rng(seed)
+    dims = MLP_SHAPE
+    ws, bs = [], []
+    for a, b in zip(dims[:-1], dims[1:]):
+        lim = np.sqrt(6.0 / (a + b))
+        ws.append(rng.uniform(-lim, lim, size=(a, b)).astype(np.float32))
+        bs.append(rng.uniform(-0.05, 0.05, size=b).astype(np.float32))
+    return ws, bs
+
+
+def to_bf16_bits(a: np.ndarray) -> np.ndarray:
+    """float32 -> bf16 bit patterns (round to nearest even), as uint16."""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    r = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return r.astype(np.uint16)
+
+
+def from_bf16_bits(b: np.ndarray) -> np.ndarray:
+    return (np.asarray(b, np.uint32) << 16).view(np.float32)

@@ -13,6 +13,14 @@ from . import abi
 from .world import TRAJ_DTYPE, ScenarioSet, WorldSpec, alloc_results
 
 
+GRID_DTYPE = np.dtype([("grid", "<i8"), ("scenarios", "<i8"), ("cost_uphmin", "<i8"),
+                       ("slo_minutes", "<i8"), ("gco2", "<f8"), ("energy_wmin", "<f8")])
+
+
+def _grid_array(a, n) -> np.ndarray:
+    return np.frombuffer(bytes(a)[:n * C.sizeof(abi.GridStats)], GRID_DTYPE).copy()
+
+
 class Engine:
     def __init__(self, device: int = 0, lib_path: str | None = None):
         self.lib = abi.load_engine(lib_path)
@@ -47,6 +55,7 @@ class Engine:
         s = sc.to_c()
         self._chk(self.lib.ccka_set_scenarios(self.ctx, C.byref(s)), "ccka_set_scenarios")
         self.n = sc.n
+        self.load_cols = sc.n_traces if sc.n_traces > 0 else sc.n
 
     def set_load(self, load: np.ndarray):
         a = np.ascontiguousarray(load, np.int32)
@@ -57,7 +66,7 @@ class Engine:
         self._chk(self.lib.ccka_gen_load(self.ctx, C.byref(gen)), "ccka_gen_load")
 
     def get_load(self) -> np.ndarray:
-        a = np.zeros((self.T, self.D, self.n), np.int32)
+        a = np.zeros((self.T, self.D, self.load_cols), np.int32)
         self._chk(self.lib.ccka_get_load(self.ctx, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size),
                   "ccka_get_load")
         return a
@@ -91,6 +100,59 @@ class Engine:
         t = abi.Totals()
         self._chk(self.lib.ccka_get_totals(self.ctx, C.byref(t)), "ccka_get_totals")
         return t
+
+    # ---- policy sweep (config 4) ----
+    def grid_stats(self, grid_size: int) -> np.ndarray:
+        ng = self.n // grid_size
+        a = (abi.GridStats * ng)()
+        self._chk(self.lib.ccka_get_grid_stats(self.ctx, C.c_int64(grid_size), a, C.c_int64(ng)),
+                  "ccka_get_grid_stats")
+        return _grid_array(a, ng)
+
+    def pareto(self, grid_size: int, capacity: int | None = None) -> np.ndarray:
+        cap = capacity if capacity is not None else max(1, self.n // grid_size) * 8
+        a = (abi.GridStats * cap)()
+        n = C.c_int32()
+        self._chk(self.lib.ccka_pareto_frontier(self.ctx, C.c_int64(grid_size), a, cap, C.byref(n)),
+                  "ccka_pareto_frontier")
+        return _grid_array(a, n.value)
+
+    # ---- learned MLP policy (config 5) ----
+    def mlp_set_weights(self, ws, bs):
+        """ws: bf16 bit arrays (uint16) [in][out]; bs: float32 biases."""
+        w = [np.ascontiguousarray(x, np.uint16) for x in ws]
+        b = [np.ascontiguousarray(x, np.float32) for x in bs]
+        u16 = C.POINTER(C.c_uint16)
+        f32 = C.POINTER(C.c_float)
+        self._chk(self.lib.ccka_mlp_set_weights(
+            self.ctx, w[0].shape[0], w[0].shape[1], w[2].shape[1],
+            w[0].ctypes.data_as(u16), b[0].ctypes.data_as(f32), w[1].ctypes.data_as(u16),
+            b[1].ctypes.data_as(f32), w[2].ctypes.data_as(u16), b[2].ctypes.data_as(f32)),
+            "ccka_mlp_set_weights")
+        self.mlp_out = w[2].shape[1]
+
+    def mlp_set_states(self, x: np.ndarray):
+        a = np.ascontiguousarray(x, np.uint16)
+        self._chk(self.lib.ccka_mlp_set_states(self.ctx, a.ctypes.data_as(C.POINTER(C.c_uint16)),
+                                               C.c_int64(a.shape[0])), "ccka_mlp_set_states")
+        self.mlp_n = a.shape[0]
+
+    def mlp_gen_states(self, n: int, seed: int = 7):
+        self._chk(self.lib.ccka_mlp_gen_states(self.ctx, C.c_int64(n), C.c_uint64(seed)),
+                  "ccka_mlp_gen_states")
+        self.mlp_n = n
+
+    def mlp_forward(self):
+        self._chk(self.lib.ccka_mlp_forward(self.ctx), "ccka_mlp_forward")
+
+    def mlp_forward_async(self):
+        self._chk(self.lib.ccka_mlp_forward_async(self.ctx), "ccka_mlp_forward_async")
+
+    def mlp_actions(self) -> np.ndarray:
+        y = np.zeros((self.mlp_n, getattr(self, "mlp_out", 8)), np.float32)
+        self._chk(self.lib.ccka_mlp_get_actions(self.ctx, y.ctypes.data_as(C.POINTER(C.c_float)),
+                                                C.c_int64(self.mlp_n)), "ccka_mlp_get_actions")
+        return y
 
     def set_engine(self, mode: int):
         """Internal: 0 = automatic engine choice, 1 = general kernel only."""

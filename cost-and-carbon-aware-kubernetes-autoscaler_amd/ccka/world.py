@@ -338,6 +338,7 @@ class WorldSpec:
 class ScenarioSet:
     n: int
     first_id: int = 0
+    n_traces: int = 0  # > 0: scenario with global id g reads shared trace g % n_traces
     region: np.ndarray | None = None
     target_util_pct: np.ndarray | None = None
     max_replicas: np.ndarray | None = None
@@ -354,7 +355,7 @@ class ScenarioSet:
 
     def to_c(self) -> abi.Scenarios:
         s = abi.Scenarios()
-        s.n, s.first_id = self.n, self.first_id
+        s.n, s.first_id, s.n_traces = self.n, self.first_id, self.n_traces
         keep = []
         for name, (npt, ct) in self._DT.items():
             a = getattr(self, name)
@@ -369,7 +370,7 @@ class ScenarioSet:
 
     def slice(self, lo, hi):
         kw = {k: (None if getattr(self, k) is None else getattr(self, k)[lo:hi]) for k in self._DT}
-        return ScenarioSet(hi - lo, self.first_id + lo, **kw)
+        return ScenarioSet(hi - lo, self.first_id + lo, self.n_traces, **kw)
 
 
 def alloc_results(n: int):

@@ -42,7 +42,7 @@ struct ccka_ctx {
   int prov[CCKA_MAX_DEPLOY] = {0};
   // scenarios
   bool have_sc = false;
-  int64_t N = 0, first_id = 0;
+  int64_t N = 0, first_id = 0, n_traces = 0;
   std::vector<uint8_t> h_region;
   uint8_t* d_region = nullptr;
   int16_t* d_target = nullptr;
@@ -88,6 +88,23 @@ struct ccka_ctx {
   int engine_mode = 0;       // 0 auto, 1 general kernel only (ccka_debug_engine)
   unsigned long long* d_stamps = nullptr;
   int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
+  // policy sweep (config 4)
+  ccka_grid_stats* d_gstats = nullptr;   // [grids] then [2 * grids] scratch
+  ccka_grid_stats* d_gcand = nullptr;
+  ccka_grid_stats* d_ggather = nullptr;
+  int64_t* d_gcounts = nullptr;
+  int32_t* d_gn = nullptr;
+  uint8_t* d_gflags = nullptr;
+  int64_t gcap = 0;
+  // learned MLP policy (config 5)
+  bool mlp_have_w = false;
+  mlp_bf16x8* d_w1f = nullptr;
+  mlp_bf16x8* d_w2f = nullptr;
+  mlp_bf16x8* d_w3f = nullptr;
+  float* d_mb = nullptr;  // b1[256] b2[256] b3[8]
+  uint16_t* d_mx = nullptr;
+  float* d_my = nullptr;
+  int64_t mlp_n = 0, mlp_cap = 0;
   int last_engine = 0;       // 1 general, 2 single-deployment
 };
 
@@ -302,7 +319,8 @@ int32_t ccka_abi_version(void) { return CCKA_ABI_VERSION; }
 int32_t ccka_struct_sizes(int64_t* out, int32_t n) {
   const int64_t s[] = {sizeof(ccka_itype),    sizeof(ccka_pool),    sizeof(ccka_deployment),
                        sizeof(ccka_world),    sizeof(ccka_scenarios), sizeof(ccka_results),
-                       sizeof(ccka_traj_rec), sizeof(ccka_totals),  sizeof(ccka_trace_gen)};
+                       sizeof(ccka_traj_rec), sizeof(ccka_totals),  sizeof(ccka_trace_gen),
+                       sizeof(ccka_grid_stats)};
   const int32_t m = (int32_t)(sizeof s / sizeof s[0]);
   int32_t k = 0;
   for (; k < m && k < n; ++k) out[k] = s[k];
@@ -362,6 +380,9 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_sinq);
   dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
+  dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_ggather); dfree(c->d_gcounts); dfree(c->d_gn);
+  dfree(c->d_gflags);
+  dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -474,6 +495,8 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   if (!c || !sc) return CCKA_EINVAL;
   if (!c->have_world) return fail(c, CCKA_ESTATE, "set_world first");
   if (sc->n < 1 || sc->n > (int64_t)1 << 31) return fail(c, CCKA_EINVAL, "scenario count out of range");
+  if (sc->n_traces < 0 || sc->n_traces > (int64_t)1 << 31 || sc->first_id < 0)
+    return fail(c, CCKA_EINVAL, "n_traces / first_id out of range");
   (void)hipSetDevice(c->device);
   const size_t n = (size_t)sc->n;
   if (sc->region) {
@@ -512,6 +535,7 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   c->d1_ready = false;
   c->N = sc->n;
   c->first_id = sc->first_id;
+  c->n_traces = sc->n_traces;
   if ((rc = alloc_results(c)) != CCKA_OK) return rc;
   dfree(c->d_load);
   c->have_load = false;
@@ -520,8 +544,10 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   return CCKA_OK;
 }
 
+static int64_t load_cols(const ccka_ctx* c) { return c->n_traces > 0 ? c->n_traces : c->N; }
+
 static int ensure_load(ccka_ctx* c) {
-  const int64_t cnt = (int64_t)c->hw.n_steps * c->hw.n_deploy * c->N;
+  const int64_t cnt = (int64_t)c->hw.n_steps * c->hw.n_deploy * load_cols(c);
   if (c->d_load && c->load_count == cnt) return CCKA_OK;
   dfree(c->d_load);
   if (hipMalloc((void**)&c->d_load, (size_t)cnt * 4) != hipSuccess)
@@ -554,8 +580,9 @@ int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
   GenParams gp{};
   gp.out = c->d_load;
   gp.sinq = c->d_sinq;
-  gp.n = c->N;
-  gp.first_id = c->first_id;
+  // shared traces are keyed by trace index, per-scenario traces by global id
+  gp.n = load_cols(c);
+  gp.first_id = c->n_traces > 0 ? 0 : c->first_id;
   gp.seed = g->seed;
   gp.T = c->hw.n_steps;
   gp.D = c->hw.n_deploy;
@@ -655,6 +682,9 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     k.traj = c->d_traj;
   }
   k.N = c->N;
+  k.NL = load_cols(c);
+  k.trace_mod = c->n_traces;
+  k.first_id = c->first_id;
   k.T = w.n_steps;
   k.D = w.n_deploy;
   k.K = w.n_types;
@@ -682,6 +712,9 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     p.peak_nodes = k.peak_nodes; p.final_reps = k.final_reps; p.final_nodes = k.final_nodes;
     p.last_choice = k.last_choice; p.hash = k.hash; p.traj = k.traj;
     p.N = c->N;
+    p.NL = k.NL;
+    p.trace_mod = k.trace_mod;
+    p.first_id = k.first_id;
     p.NW = c->NW;
     // scenarios per wave: a wave's cost is the union of its lanes' event paths,
     // so when the batch is smaller than one full round of resident waves (two
@@ -828,6 +861,219 @@ int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
   if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
     return fail(c, CCKA_ERCCL, "ncclAllReduce failed");
   HIPCHK(c, hipMemcpyAsync(io, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Policy sweep (BASELINE config 4)
+// ---------------------------------------------------------------------------
+static int sweep_grids(ccka_ctx* c, int64_t grid_size, int64_t* n_grids) {
+  if (!c->ran) return fail(c, CCKA_ESTATE, "no rollout yet");
+  if (grid_size < 1 || c->N % grid_size || c->first_id % grid_size)
+    return fail(c, CCKA_EINVAL, "batch (first_id %lld, n %lld) does not hold whole grids of %lld",
+                (long long)c->first_id, (long long)c->N, (long long)grid_size);
+  const int64_t ng = c->N / grid_size;
+  if (ng > (1 << 24)) return fail(c, CCKA_EINVAL, "too many grids");
+  if (c->gcap < ng) {
+    dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_gflags); dfree(c->d_gn);
+    if (hipMalloc((void**)&c->d_gstats, sizeof(ccka_grid_stats) * ng) != hipSuccess ||
+        hipMalloc((void**)&c->d_gcand, sizeof(ccka_grid_stats) * ng) != hipSuccess ||
+        hipMalloc((void**)&c->d_gflags, (size_t)ng) != hipSuccess ||
+        hipMalloc((void**)&c->d_gn, 2 * sizeof(int32_t)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "grid buffers");
+    c->gcap = ng;
+  }
+  GridSrc g{};
+  g.cost = c->kp.cost; g.gco2 = c->kp.gco2; g.slo = c->kp.slo; g.energy = c->kp.energy;
+  g.grid_size = grid_size;
+  g.first_grid = c->first_id / grid_size;
+  g.n_grids = ng;
+  HIPCHK(c, launch_grid_stats(g, c->d_gstats, c->stream));
+  *n_grids = ng;
+  return CCKA_OK;
+}
+
+int ccka_get_grid_stats(ccka_ctx* c, int64_t grid_size, ccka_grid_stats* out, int64_t n_grids) {
+  if (!c || !out) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  int64_t ng = 0;
+  int rc;
+  if ((rc = sweep_grids(c, grid_size, &ng)) != CCKA_OK) return rc;
+  if (n_grids != ng) return fail(c, CCKA_EINVAL, "n_grids %lld != %lld", (long long)n_grids, (long long)ng);
+  HIPCHK(c, hipMemcpyAsync(out, c->d_gstats, sizeof(ccka_grid_stats) * ng, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_pareto_frontier(ccka_ctx* c, int64_t grid_size, ccka_grid_stats* out, int32_t capacity, int32_t* n_out) {
+  if (!c || !n_out || capacity < 0 || (capacity > 0 && !out)) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  int64_t ng = 0;
+  int rc;
+  if ((rc = sweep_grids(c, grid_size, &ng)) != CCKA_OK) return rc;
+  // local frontier: non-dominated grids of this rank, in grid order
+  HIPCHK(c, launch_pareto(c->d_gstats, (int)ng, nullptr, c->d_gflags, c->d_gcand, c->d_gn, c->stream));
+  const ccka_grid_stats* front = c->d_gcand;
+  const int32_t* front_n = c->d_gn;
+  if (c->comm) {
+    // exchange: every rank's candidates (fixed capacity = grids per rank) and counts
+    int nranks = 1;
+    ncclCommCount(c->comm, &nranks);
+    dfree(c->d_ggather);
+    dfree(c->d_gcounts);
+    if (hipMalloc((void**)&c->d_ggather, sizeof(ccka_grid_stats) * ng * nranks * 2) != hipSuccess ||
+        hipMalloc((void**)&c->d_gcounts, sizeof(int64_t) * (nranks + 1)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "pareto gather buffers");
+    int64_t* cnt_local = c->d_gcounts + nranks;
+    // int32 count -> int64 slot (device copy keeps the exchange on the stream)
+    HIPCHK(c, hipMemsetAsync(cnt_local, 0, sizeof(int64_t), c->stream));
+    HIPCHK(c, hipMemcpyAsync(cnt_local, c->d_gn, sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+    ccka_grid_stats* gathered = c->d_ggather;
+    ccka_grid_stats* uni = c->d_ggather + ng * nranks;
+    uint8_t* gflags = reinterpret_cast<uint8_t*>(c->d_gstats);  // grid stats no longer needed
+    ncclGroupStart();
+    ncclResult_t r1 = ncclAllGather(cnt_local, c->d_gcounts, 1, ncclInt64, c->comm, c->stream);
+    ncclResult_t r2 = ncclAllGather(c->d_gcand, gathered, (size_t)ng * sizeof(ccka_grid_stats), ncclUint8,
+                                    c->comm, c->stream);
+    ncclResult_t r3 = ncclGroupEnd();
+    if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
+      return fail(c, CCKA_ERCCL, "ncclAllGather (pareto candidates) failed");
+    HIPCHK(c, launch_pareto_union(gathered, c->d_gcounts, nranks, (int)ng, uni, c->d_gn + 1, c->stream));
+    HIPCHK(c, launch_pareto(uni, (int)(ng * nranks), c->d_gn + 1, gflags, c->d_gcand, c->d_gn,
+                            c->stream));
+    front = c->d_gcand;
+    front_n = c->d_gn;
+  }
+  int32_t n = 0;
+  HIPCHK(c, hipMemcpyAsync(&n, front_n, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *n_out = n;
+  if (n > capacity) return fail(c, CCKA_EINVAL, "frontier has %d grids, capacity %d", n, capacity);
+  if (n > 0) {
+    HIPCHK(c, hipMemcpyAsync(out, front, sizeof(ccka_grid_stats) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return CCKA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Learned MLP policy (BASELINE config 5)
+// ---------------------------------------------------------------------------
+// MFMA fragment order of the weights (see mlp.hip). Lane l: r = l & 31, h = l >> 5.
+// Layer 1 A operand (natural k): element j = W1[16s + 8h + j][32n + r].
+// Layers 2/3 A operand, k-step kk, in the k order of the chained accumulator:
+// element j <-> input unit 32(kk>>1) + 16(kk&1) + 8(j>>2) + 4h + (j&3).
+static int kin(int kk, int j, int h) { return 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t out_dim, const uint16_t* w1,
+                         const float* b1, const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3) {
+  if (!c || !w1 || !b1 || !w2 || !b2 || !w3 || !b3) return CCKA_EINVAL;
+  if (in_dim != MLP_IN || hidden != MLP_HID || out_dim != MLP_OUT)
+    return fail(c, CCKA_EINVAL, "MLP shape %dx%dx%d unsupported (64 -> 256 -> 256 -> 8)", in_dim, hidden, out_dim);
+  (void)hipSetDevice(c->device);
+  std::vector<uint16_t> f1((size_t)8 * 4 * 64 * 8), f2((size_t)8 * 16 * 64 * 8), f3((size_t)16 * 64 * 8, 0);
+  for (int n = 0; n < 8; ++n)
+    for (int st = 0; st < 4; ++st)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int r = l & 31, h = l >> 5;
+          f1[(((size_t)n * 4 + st) * 64 + l) * 8 + j] = w1[(size_t)(16 * st + 8 * h + j) * MLP_HID + 32 * n + r];
+        }
+  for (int n = 0; n < 8; ++n)
+    for (int kk = 0; kk < 16; ++kk)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int r = l & 31, h = l >> 5;
+          f2[(((size_t)n * 16 + kk) * 64 + l) * 8 + j] = w2[(size_t)kin(kk, j, h) * MLP_HID + 32 * n + r];
+        }
+  for (int kk = 0; kk < 16; ++kk)
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) {
+        const int r = l & 31, h = l >> 5;
+        if (r < MLP_OUT) f3[((size_t)kk * 64 + l) * 8 + j] = w3[(size_t)kin(kk, j, h) * MLP_OUT + r];
+      }
+  std::vector<float> bias(MLP_HID * 2 + MLP_OUT);
+  std::memcpy(bias.data(), b1, MLP_HID * 4);
+  std::memcpy(bias.data() + MLP_HID, b2, MLP_HID * 4);
+  std::memcpy(bias.data() + 2 * MLP_HID, b3, MLP_OUT * 4);
+  int rc;
+  if ((rc = dupload(c, c->d_w1f, (const mlp_bf16x8*)f1.data(), f1.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w2f, (const mlp_bf16x8*)f2.data(), f2.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w3f, (const mlp_bf16x8*)f3.data(), f3.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_mb, bias.data(), bias.size())) != CCKA_OK) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->mlp_have_w = true;
+  return CCKA_OK;
+}
+
+static int mlp_alloc(ccka_ctx* c, int64_t n) {
+  if (n < 1 || n > ((int64_t)1 << 34)) return fail(c, CCKA_EINVAL, "state count out of range");
+  if (c->mlp_cap < n) {
+    dfree(c->d_mx);
+    dfree(c->d_my);
+    if (hipMalloc((void**)&c->d_mx, (size_t)n * MLP_IN * 2) != hipSuccess ||
+        hipMalloc((void**)&c->d_my, (size_t)n * MLP_OUT * 4) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "MLP state/action buffers (%lld states)", (long long)n);
+    c->mlp_cap = n;
+  }
+  c->mlp_n = n;
+  return CCKA_OK;
+}
+
+int ccka_mlp_set_states(ccka_ctx* c, const uint16_t* x, int64_t n) {
+  if (!c || !x) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  int rc;
+  if ((rc = mlp_alloc(c, n)) != CCKA_OK) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_mx, x, (size_t)n * MLP_IN * 2, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_mlp_gen_states(ccka_ctx* c, int64_t n, uint64_t seed) {
+  if (!c) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  int rc;
+  if ((rc = mlp_alloc(c, n)) != CCKA_OK) return rc;
+  HIPCHK(c, launch_mlp_gen_states(c->d_mx, n * MLP_IN, seed, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_mlp_forward_async(ccka_ctx* c) {
+  if (!c) return CCKA_EINVAL;
+  if (!c->mlp_have_w || !c->mlp_n) return fail(c, CCKA_ESTATE, "MLP weights / states not set");
+  (void)hipSetDevice(c->device);
+  MlpParams p{};
+  p.x = c->d_mx;
+  p.y = c->d_my;
+  p.w1f = c->d_w1f;
+  p.w2f = c->d_w2f;
+  p.w3f = c->d_w3f;
+  p.b1 = c->d_mb;
+  p.b2 = c->d_mb + MLP_HID;
+  p.b3 = c->d_mb + 2 * MLP_HID;
+  p.N = c->mlp_n;
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
+  HIPCHK(c, launch_mlp(p, c->cus, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->ran = true;
+  return CCKA_OK;
+}
+
+int ccka_mlp_forward(ccka_ctx* c) {
+  int rc = ccka_mlp_forward_async(c);
+  if (rc != CCKA_OK) return rc;
+  return ccka_sync(c);
+}
+
+int ccka_mlp_get_actions(ccka_ctx* c, float* y, int64_t n) {
+  if (!c || !y) return CCKA_EINVAL;
+  if (n != c->mlp_n) return fail(c, CCKA_EINVAL, "action count mismatch");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(y, c->d_my, (size_t)n * MLP_OUT * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return CCKA_OK;
 }

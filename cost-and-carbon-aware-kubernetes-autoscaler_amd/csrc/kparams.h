@@ -40,6 +40,9 @@ struct KParams {
   uint32_t* hash;
   ccka_traj_rec* traj;  // nullable
   int64_t N;
+  int64_t NL;           // load columns: N, or the shared trace count
+  int64_t trace_mod;    // 0: column = scenario; else column = (first_id + i) % trace_mod
+  int64_t first_id;
   int32_t T, D, K, Z, R, P, maxn, span, all_hours;
   int32_t lds_off_cap1, lds_off_tile, lds_off_claims, lds_off_misc, lds_off_ci;
   int32_t ablate;  // profiling-only phase switches (0 in every real run)
@@ -144,6 +147,7 @@ struct D1Params {
   uint32_t* hash;
   ccka_traj_rec* traj;  // nullable
   int64_t N;
+  int64_t NL, trace_mod, first_id;  // load columns / shared-trace mapping (as KParams)
   int32_t lpw;  // scenarios per wave (<= 64; fewer lanes = less divergence per wave)
   int32_t T, K, Z, R, NP, maxn, NZI, NW, JT;
   int32_t start_minute, peak_start, peak_end, pswitch0, delay;
@@ -173,6 +177,42 @@ struct TableParams {
 };
 
 hipError_t launch_table(const TableParams& t, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Policy sweep (config 4): per-grid sums and the Pareto frontier (sweep.hip)
+// ---------------------------------------------------------------------------
+struct GridSrc {
+  const int64_t* cost;
+  const double* gco2;
+  const int32_t* slo;
+  const double* energy;
+  int64_t grid_size, first_grid, n_grids;
+};
+hipError_t launch_grid_stats(const GridSrc& g, ccka_grid_stats* out, hipStream_t s);
+// non-dominated entries of in[0..n) (n may be device-resident: *n_dev if n < 0),
+// compacted in input order into out; count into *count_dev
+hipError_t launch_pareto(const ccka_grid_stats* in, int n, const int32_t* n_dev, uint8_t* flags,
+                         ccka_grid_stats* out, int32_t* count_dev, hipStream_t s);
+// concatenate the valid prefixes of an all-gathered [ranks][cap] buffer
+hipError_t launch_pareto_union(const ccka_grid_stats* gathered, const int64_t* counts, int ranks, int cap,
+                               ccka_grid_stats* out, int32_t* n_dev, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Learned MLP policy (config 5, mlp.hip)
+// ---------------------------------------------------------------------------
+constexpr int MLP_IN = 64, MLP_HID = 256, MLP_OUT = 8;
+typedef short mlp_bf16x8 __attribute__((ext_vector_type(8)));
+struct MlpParams {
+  const uint16_t* x;          // [N][64] bf16
+  float* y;                   // [N][8]
+  const mlp_bf16x8* w1f;      // [8 row tiles][4 k-steps][64 lanes] A fragments of layer 1
+  const mlp_bf16x8* w2f;      // [8][16][64] (k order of the chained accumulator)
+  const mlp_bf16x8* w3f;      // [16][64], rows 8..31 zero
+  const float *b1, *b2, *b3;
+  int64_t N;
+};
+hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s);
+hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipStream_t s);
 hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s);
 
 }  // namespace ccka

@@ -484,8 +484,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   // load samples are software-pipelined one step ahead: the HBM latency of
   // step t+1's coalesced read hides behind step t's decision work
   int Lnext[DMAX];
-  const int32_t* lptr = p.load + (active ? i : 0);
-  const int64_t lstride = p.N;
+  // load column: the scenario's own trace, or its shared trace (policy sweeps)
+  const int64_t lcol = !active ? 0 : (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
+  const int32_t* lptr = p.load + lcol;
+  const int64_t lstride = p.NL;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) Lnext[d] = lptr[(d < D ? d : 0) * lstride];
   int minute = gw->start_minute % 1440;

@@ -406,7 +406,9 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
 
   // load samples software-pipelined one step ahead: a step is long enough to
   // cover the HBM latency of the next step's coalesced read
-  const int32_t* lp = p.load + i;
+  // load column: the scenario's own trace, or its shared trace (policy sweeps)
+  const int32_t* lp = p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
+  const long long lsl = opq(p.NL);
   // Memory pipeline of one step: at its top the previous step's trajectory
   // record is stored and the next step's load sample is issued; the sample is
   // taken into a register only at the end of the step, so every wait the
@@ -417,7 +419,7 @@ __global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
 
   for (int t = 0; t < T; ++t, minute = minute == 1439 ? 0 : minute + 1) {
     if (traj && t > 0) *(int4*)(traj + (int64_t)(t - 1) * ls + i) = rec_prev;
-    const int Lraw = lp[(int64_t)min(t + 1, T - 1) * ls];
+    const int Lraw = lp[(int64_t)min(t + 1, T - 1) * lsl];
     const int L = Lcur;
     const int h = minute / 60;
     const int rh = r * 24 + h;

@@ -166,6 +166,10 @@ typedef struct ccka_world {
 typedef struct ccka_scenarios {
   int64_t n;
   int64_t first_id;             /* global id of element 0 (trace RNG key) */
+  int64_t n_traces;             /* 0: one load trace per scenario ([T][D][n]);
+                                   > 0: a shared trace set [T][D][n_traces], scenario
+                                   with global id g reads trace g mod n_traces (policy
+                                   sweeps: every parameter grid over the same traces) */
   const uint8_t* region;
   const int16_t* target_util_pct;
   const int16_t* max_replicas;
@@ -219,6 +223,17 @@ typedef struct ccka_totals {
   double gco2;
 } ccka_totals;
 
+/* Per-grid sums of a policy sweep (BASELINE config 4): grid g = the scenarios
+ * with global ids [g*grid_size, (g+1)*grid_size). 48 bytes. */
+typedef struct ccka_grid_stats {
+  int64_t grid;
+  int64_t scenarios;
+  int64_t cost_uphmin;
+  int64_t slo_minutes;
+  double gco2;
+  double energy_wmin;
+} ccka_grid_stats;
+
 /* Synthetic load-trace generator (docs/SEMANTICS.md §4). */
 typedef struct ccka_trace_gen {
   uint64_t seed;
@@ -267,6 +282,36 @@ int ccka_last_kernel_ms(ccka_ctx* ctx, double* ms);
 int ccka_get_results(ccka_ctx* ctx, ccka_results* out);
 int ccka_get_trajectory(ccka_ctx* ctx, ccka_traj_rec* out, int64_t count);
 int ccka_get_totals(ccka_ctx* ctx, ccka_totals* out);
+
+/* ---- policy sweep (BASELINE config 4) -------------------------------- */
+/* Per-grid sums of the last rollout's results. The batch must hold whole
+ * grids (first_id and n multiples of grid_size); out[n / grid_size]. Sums are
+ * taken on the device in a fixed order (deterministic). */
+int ccka_get_grid_stats(ccka_ctx* ctx, int64_t grid_size, ccka_grid_stats* out, int64_t n_grids);
+/* Cost / gCO2 / SLO-minutes Pareto frontier of the batch's grids (all three
+ * minimised; equal vectors do not dominate each other). With a communicator
+ * (ccka_comm_init) each rank's non-dominated grids are exchanged with an RCCL
+ * all-gather over xGMI and every rank filters the union the same way, so all
+ * ranks return the identical global frontier, sorted by grid id. Writes at most
+ * `capacity` entries; *n_out = frontier size (CCKA_EINVAL if it exceeds
+ * capacity). Every rank must hold the same number of grids. */
+int ccka_pareto_frontier(ccka_ctx* ctx, int64_t grid_size, ccka_grid_stats* out, int32_t capacity,
+                         int32_t* n_out);
+
+/* ---- learned MLP control policy (BASELINE config 5) ------------------- */
+/* Weights of the state(64) -> 256 -> 256 -> actions(8) ReLU policy: bf16 bit
+ * patterns, row-major [in][out]; biases fp32. Only that shape is supported. */
+int ccka_mlp_set_weights(ccka_ctx* ctx, int32_t in_dim, int32_t hidden, int32_t out_dim,
+                         const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                         const uint16_t* w3, const float* b3);
+/* Cluster states [n][in_dim] bf16: uploaded, or synthesised on the device. */
+int ccka_mlp_set_states(ccka_ctx* ctx, const uint16_t* x, int64_t n);
+int ccka_mlp_gen_states(ccka_ctx* ctx, int64_t n, uint64_t seed);
+/* actions = policy(states) on the device (bf16 MFMA, fp32 accumulation). */
+int ccka_mlp_forward(ccka_ctx* ctx);
+int ccka_mlp_forward_async(ccka_ctx* ctx);
+/* Copy the actions [n][out_dim] fp32 back. */
+int ccka_mlp_get_actions(ccka_ctx* ctx, float* y, int64_t n);
 
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------- */
 /* Fill a 128-byte RCCL unique id (rank 0 only; distribute it out of band). */

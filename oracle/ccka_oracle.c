@@ -330,6 +330,9 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
   const int D = e->D, NN = e->N, K = e->K;
   o_state st;
   memset(&st, 0, sizeof st);
+  /* load column: the scenario's own trace, or its shared trace (policy sweeps) */
+  const int64_t nl = sc->n_traces > 0 ? sc->n_traces : nsc;
+  const int64_t col = sc->n_traces > 0 ? (sc->first_id + i) % sc->n_traces : i;
   const int r = sc->region ? sc->region[i] : 0;
   const int reset_ca = sc->reset_ca_s ? sc->reset_ca_s[i] : w->reset_ca_s;
   const int pswitch = sc->peak_switch ? sc->peak_switch[i] : w->peak_switch;
@@ -394,7 +397,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     for (int d = 0; d < D; ++d) {
       const ccka_deployment* dp = &w->deploy[d];
       o_dep* ds = &st.dep[d];
-      const int64_t L = load[((int64_t)t * D + d) * nsc + i];
+      const int64_t L = load[((int64_t)t * D + d) * nl + col];
       Lt[d] = L;
       util_valid[d] = 0;
       util[d] = 0;

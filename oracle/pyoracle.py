@@ -69,7 +69,8 @@ def rollout(spec, scen, load, traj=False, threads=1):
     w = spec.to_c()
     s = scen.to_c()
     load = np.ascontiguousarray(load, np.int32)
-    assert load.shape == (spec.n_steps, len(spec.deploys), scen.n), load.shape
+    cols = scen.n_traces if scen.n_traces > 0 else scen.n
+    assert load.shape == (spec.n_steps, len(spec.deploys), cols), load.shape
     arrays, r = alloc_results(scen.n)
     tr = None
     trp = None
@@ -107,3 +108,40 @@ def rollout_world(world, scen, load, traj=False, threads=1):
     if rc != 0:
         raise abi.CckaError(f"oracle rollout failed: {rc}")
     return arrays, tr
+
+
+# ---------------------------------------------------------------------------
+# Policy sweep (BASELINE config 4): per-grid sums and the Pareto frontier,
+# restated in numpy (minimise cost, gCO2 and SLO-minutes;
+# a grid is dropped iff another grid is <= in all three and < in one).
+# ---------------------------------------------------------------------------
+def grid_stats(res, grid_size, first_id=0):
+    """Per-grid sums of oracle results (ints exact; doubles summed in index order)."""
+    n = len(res["cost_uphmin"])
+    assert n % grid_size == 0 and first_id % grid_size == 0
+    ng = n // grid_size
+    sh = (ng, grid_size)
+    return {
+        "grid": np.arange(first_id // grid_size, first_id // grid_size + ng, dtype=np.int64),
+        "scenarios": np.full(ng, grid_size, np.int64),
+        "cost_uphmin": res["cost_uphmin"].reshape(sh).sum(axis=1),
+        "slo_minutes": res["slo_minutes"].astype(np.int64).reshape(sh).sum(axis=1),
+        "gco2": res["gco2"].reshape(sh).sum(axis=1),
+        "energy_wmin": res["energy_wmin"].reshape(sh).sum(axis=1),
+    }
+
+
+def pareto(stats):
+    """Indices (ascending) of the non-dominated grids."""
+    c = np.asarray(stats["cost_uphmin"])
+    g = np.asarray(stats["gco2"])
+    s = np.asarray(stats["slo_minutes"])
+    keep = []
+    for i in range(len(c)):
+        le = (c <= c[i]) & (g <= g[i]) & (s <= s[i])
+        lt = (c < c[i]) | (g < g[i]) | (s < s[i])
+        dom = le & lt
+        dom[i] = False
+        if not dom.any():
+            keep.append(i)
+    return np.array(keep, dtype=np.int64)

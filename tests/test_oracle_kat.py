@@ -246,3 +246,48 @@ def test_oracle_deterministic_and_thread_invariant():
     for k in a:
         assert np.array_equal(a[k], b[k]), k
     assert np.array_equal(ta, tb)
+
+
+# ---------------------------------------------------------------- energy (SEMANTICS §3.H)
+def test_energy_integer_nanowatt_minutes():
+    """One scenario, constant load, no scaling: the step energy is exactly
+    base + idle + dyn_per_m * min(pods * upp, alloc) in nW (hand-derived)."""
+    spec = configs.config2_world(n_steps=3)
+    spec.deploys = [deployment(abi.SCALER_STATIC, replicas0=2, min_r=2, max_r=2, limit_cpu=0)]
+    spec.peak_switch = 0
+    spec.provision_delay_steps = 0
+    sc = ScenarioSet(1)
+    load = np.full((3, 1, 1), 301, np.int32)
+    res, tr = po.rollout(spec, sc, load, traj=True)
+    types = spec.catalog.itypes()
+    bt = types[spec.catalog.index("m6i.large")]
+    base = spec.base_nodes * (bt.idle_nw + bt.dyn_nw_per_m * int(spec.base_util * bt.alloc_cpu_m))
+    k = res["last_choice"][0] & 0xFFF
+    ty = types[int(k)]
+    upp = 301 // 2
+    step = base + ty.idle_nw + ty.dyn_nw_per_m * min(2 * upp, ty.alloc_cpu_m)
+    assert res["energy_wmin"][0] == float(3 * step) * 1e-9
+    ci = spec.ci[0, 0] / 60000.0
+    assert res["gco2"][0] == float(3 * step) * (ci * 1e-9)
+
+
+def test_shared_traces_equal_expanded_traces():
+    """n_traces > 0 reads trace (first_id + i) % n_traces: identical to giving
+    every scenario a copy of its trace."""
+    spec = configs.config2_world(n_steps=120)
+    sc = configs.config4_scenarios(3, 4, 16)
+    shared = po.gen_load(configs.config4_trace_gen(), 120, 1, 16)
+    r1, _ = po.rollout(spec, sc, shared, threads=4)
+    sc2 = configs.config4_scenarios(3, 4, 16)
+    sc2.n_traces = 0
+    cols = (sc.first_id + np.arange(sc.n)) % 16
+    r2, _ = po.rollout(spec, sc2, np.ascontiguousarray(shared[:, :, cols]), threads=4)
+    for f in r1:
+        assert np.array_equal(r1[f], r2[f]), f
+
+
+def test_pareto_known_answer():
+    st = {"cost_uphmin": np.array([5, 3, 4, 3, 6]), "gco2": np.array([1.0, 2.0, 2.0, 2.0, 0.5]),
+          "slo_minutes": np.array([0, 0, 0, 1, 9])}
+    # 2 is dominated by 1 (equal carbon/SLO, cheaper); 3 by 1; 1 == itself kept
+    assert po.pareto(st).tolist() == [0, 1, 4]
