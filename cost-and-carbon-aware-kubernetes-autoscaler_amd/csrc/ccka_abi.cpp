@@ -88,6 +88,7 @@ struct ccka_ctx {
   int engine_mode = 0;       // 0 auto, 1 general kernel only (ccka_debug_engine)
   unsigned long long* d_stamps = nullptr;
   int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
+  int occ = 0;               // its register-allocation occupancy target (0 = automatic)
   // policy sweep (config 4)
   ccka_grid_stats* d_gstats = nullptr;   // [grids] then [2 * grids] scratch
   ccka_grid_stats* d_gcand = nullptr;
@@ -719,6 +720,11 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     // scenarios per wave: a wave's cost is the union of its lanes' event paths,
     // so when the batch is smaller than one full round of resident waves (two
     // per SIMD at this kernel's register budget) spread it over all of them
+    {
+      const int64_t waves = (c->N + 63) / 64, round = 2LL * 4 * c->cus;
+      p.occ = c->occ > 0 ? c->occ : 2;  // higher targets spill (measured slower: tools/occ.py)
+      (void)waves; (void)round;
+    }
     if (c->lpw > 0) {
       p.lpw = c->lpw;
     } else {
@@ -1107,6 +1113,13 @@ int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
 int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
   if (!c || lpw < 0 || lpw > 64) return CCKA_EINVAL;
   c->lpw = lpw;
+  return CCKA_OK;
+}
+
+// Internal: occupancy target of the single-deployment kernel (2, 3, 4; 0 = automatic).
+int ccka_debug_occ(ccka_ctx* c, int32_t occ) {
+  if (!c || occ < 0 || occ > 4 || occ == 1) return CCKA_EINVAL;
+  c->occ = occ;
   return CCKA_OK;
 }
 

@@ -149,6 +149,7 @@ struct D1Params {
   int64_t N;
   int64_t NL, trace_mod, first_id;  // load columns / shared-trace mapping (as KParams)
   int32_t lpw;  // scenarios per wave (<= 64; fewer lanes = less divergence per wave)
+  int32_t occ;  // register-allocation occupancy target of the instantiation (2, 3 or 4)
   int32_t T, K, Z, R, NP, maxn, NZI, NW, JT;
   int32_t start_minute, peak_start, peak_end, pswitch0, delay;
   int32_t base_nodes, base_type, slo_util, pdb_pct, pdb_member;

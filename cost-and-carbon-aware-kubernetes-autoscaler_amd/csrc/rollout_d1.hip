@@ -265,13 +265,15 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 // cycle totals summed over waves into p.stamps[8].
 #define D1_STAMP(k)                                          \
   if constexpr (STAMPS) {                                    \
+    __builtin_amdgcn_sched_barrier(0);                       \
     const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+    __builtin_amdgcn_sched_barrier(0);                       \
     st_acc[k] += now_ - st_last;                             \
     st_last = now_;                                          \
   }
 
-template <int MAXN, int MAXP, bool STAMPS>
-__global__ void __launch_bounds__(256) rollout_d1_kernel(D1Params p) {
+template <int MAXN, int MAXP, bool STAMPS, int OCC>
+__global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   // per instance type: {idle_nw lo, idle_nw hi, dyn_nw_per_m, alloc_cpu_m} (one ds_read_b128)
@@ -892,16 +894,23 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const int64_t waves = (p.N + p.lpw - 1) / p.lpw;
   const unsigned grid = (unsigned)((waves + B / WAVE - 1) / (B / WAVE));
   const size_t lds = (size_t)p.K * sizeof(int4);
+  // OCC = resident waves per SIMD the register allocation targets: 2 (no
+  // spills) when the batch is a single round of waves, 3 for multi-round
+  // batches (configs 3/4), where more resident waves hide more latency
   if (p.stamps)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2>), dim3(grid), dim3(B), lds, s, p);
+  else if (p.maxn <= 8 && p.NP <= 2 && p.occ >= 4)
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 4>), dim3(grid), dim3(B), lds, s, p);
+  else if (p.maxn <= 8 && p.NP <= 2 && p.occ == 3)
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 3>), dim3(grid), dim3(B), lds, s, p);
   else if (p.maxn <= 8 && p.NP <= 2)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2>), dim3(grid), dim3(B), lds, s, p);
   else if (p.maxn <= 8)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false, 2>), dim3(grid), dim3(B), lds, s, p);
   else if (p.NP <= 2)
-    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false, 1>), dim3(grid), dim3(B), lds, s, p);
   else
-    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false, 1>), dim3(grid), dim3(B), lds, s, p);
   return hipGetLastError();
 }
 
