@@ -32,13 +32,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int WAVE = 64;
 
-// ReLU, then registers 8s..8s+7 as one bf16 operand fragment (round to nearest even)
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+// registers 8s..8s+7 as one bf16 operand fragment with ReLU: pairs rounded to
+// nearest even (v_cvt_pk_bf16_f32), then ReLU on the bf16 bit patterns as
+// packed int16 max with 0 (v_pk_max_i16: every negative value, -0 included,
+// has the sign bit set) -- the same bits as rounding relu(x)
 __device__ __forceinline__ bf16x8 relu_pack(const f32x16& a, int s) {
   bf16x8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 b = (__bf16)fmaxf(a[8 * s + j], 0.0f);
-    r[j] = __builtin_bit_cast(short, b);
+  for (int j = 0; j < 8; j += 2) {
+    const bf16x2v b = __builtin_convertvector((f32x2){a[8 * s + j], a[8 * s + j + 1]}, bf16x2v);
+    const short2v v = __builtin_elementwise_max(__builtin_bit_cast(short2v, b), (short2v){0, 0});
+    r[j] = v.x;
+    r[j + 1] = v.y;
   }
   return r;
 }
@@ -64,9 +73,9 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 }  // namespace
 
 __global__ void __launch_bounds__(256, 1) mlp_kernel(MlpParams p) {
-  __shared__ bf16x8 s_w2[MLP_HID / 32 * (MLP_HID / 16) * WAVE];  // 128 KiB
-  __shared__ bf16x8 s_w3[(MLP_HID / 16) * WAVE];                  // 16 KiB
   __shared__ __attribute__((aligned(16))) float s_b1[MLP_HID], s_b2[MLP_HID], s_b3[32];
+  __shared__ bf16x8 s_w3[(MLP_HID / 16) * WAVE];                  // 16 KiB
+  __shared__ bf16x8 s_w2[MLP_HID / 32 * (MLP_HID / 16) * WAVE];  // 128 KiB
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
   const int r = lane & 31, h = lane >> 5;
   for (int x = tid; x < MLP_HID / 32 * (MLP_HID / 16) * WAVE; x += blockDim.x) s_w2[x] = p.w2f[x];
@@ -78,7 +87,10 @@ __global__ void __launch_bounds__(256, 1) mlp_kernel(MlpParams p) {
 #pragma unroll
   for (int n = 0; n < MLP_HID / 32; ++n)
 #pragma unroll
-    for (int s = 0; s < MLP_IN / 16; ++s) w1[n][s] = p.w1f[(n * (MLP_IN / 16) + s) * WAVE + lane];
+    for (int s = 0; s < MLP_IN / 16; ++s) {
+      w1[n][s] = p.w1f[(n * (MLP_IN / 16) + s) * WAVE + lane];
+      asm volatile("" : "+a"(w1[n][s]));  // accumulation registers: MFMA reads its A operand from them
+    }
   __syncthreads();
 
   const int64_t ntiles = (p.N + 31) / 32;
@@ -100,40 +112,56 @@ __global__ void __launch_bounds__(256, 1) mlp_kernel(MlpParams p) {
   for (; tile < ntiles; tile += nw) {
     load_x(tile + nw, xn);  // next tile in flight during this tile's MFMAs
     // ---- layer 1: H1^T = relu(W1^T X^T + b1) ----
+    // row blocks software-pipelined: block n+1's MFMAs are issued before
+    // block n's ReLU/bf16 epilogue, which then runs in their shadow
     bf16x8 hf[MLP_HID / 16];
+    f32x16 acur = bias_tile(s_b1, h);
+#pragma unroll
+    for (int s = 0; s < MLP_IN / 16; ++s) acur = mfma(w1[0][s], xf[s], acur);
 #pragma unroll
     for (int n = 0; n < MLP_HID / 32; ++n) {
-      f32x16 a = bias_tile(s_b1 + 32 * n, h);
+      f32x16 anext;
+      if (n + 1 < MLP_HID / 32) {
+        anext = bias_tile(s_b1 + 32 * (n + 1), h);
 #pragma unroll
-      for (int s = 0; s < MLP_IN / 16; ++s) a = mfma(w1[n][s], xf[s], a);
-      hf[2 * n] = relu_pack(a, 0);
-      hf[2 * n + 1] = relu_pack(a, 1);
+        for (int s = 0; s < MLP_IN / 16; ++s) anext = mfma(w1[n + 1][s], xf[s], anext);
+      }
+      hf[2 * n] = relu_pack(acur, 0);
+      hf[2 * n + 1] = relu_pack(acur, 1);
+      if (n + 1 < MLP_HID / 32) acur = anext;
     }
     // ---- layer 2: H2^T = relu(W2^T H1^T + b2) ----
     f32x16 a2[MLP_HID / 32];
 #pragma unroll
     for (int n = 0; n < MLP_HID / 32; ++n) a2[n] = bias_tile(s_b2 + 32 * n, h);
+    // W2 fragments software-pipelined one k-step ahead (LDS latency hidden
+    // behind the current k-step's 8 MFMAs); the barriers keep exactly two
+    // k-steps of fragments in registers (the scheduler would otherwise hoist
+    // all 128 fragment reads and spill)
+    bf16x8 wf[MLP_HID / 32], wn[MLP_HID / 32];
+#pragma unroll
+    for (int n = 0; n < MLP_HID / 32; ++n) wf[n] = s_w2[n * (MLP_HID / 16) * WAVE + lane];
 #pragma unroll
     for (int kk = 0; kk < MLP_HID / 16; ++kk) {
-      bf16x8 wf[MLP_HID / 32];
+      if (kk + 1 < MLP_HID / 16) {
 #pragma unroll
-      for (int n = 0; n < MLP_HID / 32; ++n) wf[n] = s_w2[(n * (MLP_HID / 16) + kk) * WAVE + lane];
+        for (int n = 0; n < MLP_HID / 32; ++n) wn[n] = s_w2[(n * (MLP_HID / 16) + kk + 1) * WAVE + lane];
+      }
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int n = 0; n < MLP_HID / 32; ++n) a2[n] = mfma(wf[n], hf[kk], a2[n]);
-      // keep one k-step of W2 fragments in flight at a time (the scheduler
-      // would otherwise hoist all 128 fragment reads and spill)
-      asm volatile("" ::: "memory");
-    }
-    bf16x8 gf[MLP_HID / 16];
 #pragma unroll
-    for (int n = 0; n < MLP_HID / 32; ++n) {
-      gf[2 * n] = relu_pack(a2[n], 0);
-      gf[2 * n + 1] = relu_pack(a2[n], 1);
+      for (int n = 0; n < MLP_HID / 32; ++n) wf[n] = wn[n];
     }
     // ---- layer 3: Y^T = W3^T H2^T + b3 (rows 8..31 of W3^T are zero) ----
+    // interleaved with layer 2's epilogue: k-steps 2n, 2n+1 need only block n
     f32x16 a3 = bias_tile(s_b3, h);
 #pragma unroll
-    for (int kk = 0; kk < MLP_HID / 16; ++kk) a3 = mfma(s_w3[kk * WAVE + lane], gf[kk], a3);
+    for (int n = 0; n < MLP_HID / 32; ++n) {
+      const bf16x8 g0 = relu_pack(a2[n], 0), g1 = relu_pack(a2[n], 1);
+      a3 = mfma(s_w3[(2 * n) * WAVE + lane], g0, a3);
+      a3 = mfma(s_w3[(2 * n + 1) * WAVE + lane], g1, a3);
+    }
     // registers 0..3 hold outputs 4h..4h+3 of state r
     const int64_t row = tile * 32 + r;
     if (row < p.N) *reinterpret_cast<f32x4*>(p.y + row * MLP_OUT + 4 * h) = f32x4{a3[0], a3[1], a3[2], a3[3]};

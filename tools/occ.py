@@ -11,6 +11,10 @@ from ccka.engine import Engine  # noqa: E402
 
 eng = Engine(0)
 eng.lib.ccka_debug_occ.argtypes = [C.c_void_p, C.c_int32]
+eng.lib.ccka_debug_lpw.argtypes = [C.c_void_p, C.c_int32]
+# config 2 is one resident round at 2 waves/SIMD: refill the round for the
+# occupancy being tested (lanes per wave = N / (occ * 4 SIMDs * CUs))
+LPW2 = {2: 0, 3: 33, 4: 25}
 cases = {
     "config2": (configs.config2_world(), configs.hpa_scenarios(100_000), configs.trace_gen(), True),
     "config3": (configs.config3_world(), configs.config3_scenarios(1_000_000), configs.trace_gen(), False),
@@ -25,6 +29,7 @@ for name, (spec, sc, gen, traj) in cases.items():
     for r in range(2):
         for occ in (2, 3, 4):
             eng.lib.ccka_debug_occ(eng.ctx, occ)
+            eng.lib.ccka_debug_lpw(eng.ctx, LPW2[occ] if name == "config2" else 0)
             eng.rollout(trajectory=traj)
             res.setdefault(occ, []).append(eng.kernel_ms())
             out = eng.results()
