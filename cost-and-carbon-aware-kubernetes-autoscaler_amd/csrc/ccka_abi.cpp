@@ -89,6 +89,7 @@ struct ccka_ctx {
   unsigned long long* d_stamps = nullptr;
   int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
   int occ = 0;               // its register-allocation occupancy target (0 = automatic)
+  int mlp_stamps = 0;        // diagnostic MLP phase stamps (ccka_debug_mlp_stamps)
   // policy sweep (config 4)
   ccka_grid_stats* d_gstats = nullptr;   // [grids] then [2 * grids] scratch
   ccka_grid_stats* d_gcand = nullptr;
@@ -999,7 +1000,7 @@ int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t ou
         const int r = l & 31, h = l >> 5;
         if (r < MLP_OUT) f3[((size_t)kk * 64 + l) * 8 + j] = w3[(size_t)kin(kk, j, h) * MLP_OUT + r];
       }
-  std::vector<float> bias(MLP_HID * 2 + MLP_OUT);
+  std::vector<float> bias(MLP_HID * 2 + 32);  // b3 zero-padded to one 32-row tile
   std::memcpy(bias.data(), b1, MLP_HID * 4);
   std::memcpy(bias.data() + MLP_HID, b2, MLP_HID * 4);
   std::memcpy(bias.data() + 2 * MLP_HID, b3, MLP_OUT * 4);
@@ -1061,6 +1062,13 @@ int ccka_mlp_forward_async(ccka_ctx* c) {
   p.b2 = c->d_mb + MLP_HID;
   p.b3 = c->d_mb + 2 * MLP_HID;
   p.N = c->mlp_n;
+  p.stamps = nullptr;
+  if (c->mlp_stamps) {
+    if (!c->d_stamps && hipMalloc((void**)&c->d_stamps, 12 * sizeof(unsigned long long)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "stamps alloc");
+    HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, 12 * sizeof(unsigned long long), c->stream));
+    p.stamps = c->d_stamps;
+  }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
   HIPCHK(c, launch_mlp(p, c->cus, c->stream));
@@ -1124,6 +1132,13 @@ int ccka_debug_occ(ccka_ctx* c, int32_t occ) {
 }
 
 // Internal: per-phase cycle totals of the last stamped rollout (ablate bit 16).
+// Internal: diagnostic phase stamps of the MLP kernel (read with ccka_debug_stamps).
+int ccka_debug_mlp_stamps(ccka_ctx* c, int32_t enable) {
+  if (!c) return CCKA_EINVAL;
+  c->mlp_stamps = enable != 0;
+  return CCKA_OK;
+}
+
 int ccka_debug_stamps(ccka_ctx* c, unsigned long long* out8) {
   if (!c || !out8 || !c->d_stamps) return CCKA_EINVAL;
   HIPCHK(c, hipMemcpy(out8, c->d_stamps, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));

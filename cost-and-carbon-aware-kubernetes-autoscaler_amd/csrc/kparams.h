@@ -211,6 +211,7 @@ struct MlpParams {
   const mlp_bf16x8* w3f;      // [16][64], rows 8..31 zero
   const float *b1, *b2, *b3;
   int64_t N;
+  unsigned long long* stamps;  // diagnostic phase stamps (nullptr in every real run)
 };
 hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s);
 hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipStream_t s);

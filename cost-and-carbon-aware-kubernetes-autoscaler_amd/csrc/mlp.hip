@@ -12,11 +12,17 @@
 // the weight fragments out in exactly that order (ccka_abi.cpp,
 // mlp_fragments), so no activation ever moves between lanes or through LDS.
 //
-// Residency: W1 fragments (32 KB) live in each wave's registers, W2 (128 KB)
-// and W3 (16 KB, rows 8..31 zero) fragments plus the biases in LDS; one
-// persistent 4-wave workgroup per CU, each wave streaming 32-state tiles of X
-// from HBM with the next tile's loads in flight during the current tile's
-// 176 MFMAs.
+// Residency and schedule (one persistent 4-wave workgroup per CU, one wave
+// per SIMD): W1 fragments (32 KiB) in each wave's accumulation registers, W2
+// and W3 fragments and the biases (146 KiB) in LDS; MFMA accumulators in
+// architectural VGPRs (built with -amdgpu-mfma-vgpr-form) so the packed
+// ReLU/bf16 epilogue reads them directly. Each wave evaluates two 32-state
+// tiles per pass (every LDS fragment feeds two MFMAs); layer-1 row blocks and
+// layer-2 row blocks are software-pipelined so each block's epilogue runs in
+// the shadow of the next block's MFMAs. Measured (tools/mlp_stamps.py): 77 %
+// of the MFMA-issue floor in cycles; under this kernel's power draw the shader
+// clock settles near 1.8 GHz (tools/probe/clockprobe: 2.24 GHz for a
+// low-toggle MFMA stream).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -52,7 +58,8 @@ __device__ __forceinline__ bf16x8 relu_pack(const f32x16& a, int s) {
   return r;
 }
 
-// accumulator initialised with the bias of its rows: row = (reg&3) + 8(reg>>2) + 4h
+// accumulator tile of the bias of rows 32 blocks: row = (reg&3) + 8(reg>>2) + 4h
+// (four 16-byte loads, L1/L2-resident; used as the C operand of the first MFMA)
 __device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
   f32x16 a;
 #pragma unroll
@@ -72,101 +79,182 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
 
 }  // namespace
 
+// One persistent 4-wave workgroup per CU. W1 fragments (32 KiB) live in each
+// wave's accumulation registers; W2 and W3 fragments and the biases
+// (146 KiB) in LDS. Each wave evaluates TWO 32-state tiles per pass, so every
+// W2 / W3 fragment and bias tile read from LDS feeds two MFMAs and the two
+// tiles' dependency chains interleave.
+// STAMPS: diagnostic build only: s_memtime cycle totals of layer 1 and of
+// layers 2+3 summed over waves into p.stamps[0..1]
+template <bool STAMPS>
 __global__ void __launch_bounds__(256, 1) mlp_kernel(MlpParams p) {
-  __shared__ __attribute__((aligned(16))) float s_b1[MLP_HID], s_b2[MLP_HID], s_b3[32];
-  __shared__ bf16x8 s_w3[(MLP_HID / 16) * WAVE];                  // 16 KiB
-  __shared__ bf16x8 s_w2[MLP_HID / 32 * (MLP_HID / 16) * WAVE];  // 128 KiB
+  unsigned long long st[2] = {0, 0}, st_last = 0;
+  const unsigned long long k0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0, r0 = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+  constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
+  __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 32];  // b1 | b2 | b3 (zero-padded)
+  __shared__ bf16x8 s_w3[KS2 * WAVE];                                   // 16 KiB
+  __shared__ bf16x8 s_w2[NB * KS2 * WAVE];                              // 128 KiB
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
   const int r = lane & 31, h = lane >> 5;
-  for (int x = tid; x < MLP_HID / 32 * (MLP_HID / 16) * WAVE; x += blockDim.x) s_w2[x] = p.w2f[x];
-  for (int x = tid; x < (MLP_HID / 16) * WAVE; x += blockDim.x) s_w3[x] = p.w3f[x];
-  for (int x = tid; x < MLP_HID; x += blockDim.x) { s_b1[x] = p.b1[x]; s_b2[x] = p.b2[x]; }
-  if (tid < 32) s_b3[tid] = tid < MLP_OUT ? p.b3[tid] : 0.0f;
-  // layer-1 weight fragments stay in registers for the whole kernel
-  bf16x8 w1[MLP_HID / 32][MLP_IN / 16];
+  for (int x = tid; x < NB * KS2 * WAVE; x += blockDim.x) s_w2[x] = p.w2f[x];
+  for (int x = tid; x < KS2 * WAVE; x += blockDim.x) s_w3[x] = p.w3f[x];
+  for (int x = tid; x < 2 * MLP_HID + 32; x += blockDim.x) s_b[x] = p.b1[x];  // b1, b2, b3 are contiguous
+  bf16x8 w1[NB][KS1];
 #pragma unroll
-  for (int n = 0; n < MLP_HID / 32; ++n)
+  for (int n = 0; n < NB; ++n)
 #pragma unroll
-    for (int s = 0; s < MLP_IN / 16; ++s) {
-      w1[n][s] = p.w1f[(n * (MLP_IN / 16) + s) * WAVE + lane];
+    for (int s = 0; s < KS1; ++s) {
+      w1[n][s] = p.w1f[(n * KS1 + s) * WAVE + lane];
       asm volatile("" : "+a"(w1[n][s]));  // accumulation registers: MFMA reads its A operand from them
     }
   __syncthreads();
+  const float* const s_b1 = s_b;
+  const float* const s_b2 = s_b + MLP_HID;
+  const float* const s_b3 = s_b + 2 * MLP_HID;
 
-  const int64_t ntiles = (p.N + 31) / 32;
+  const int64_t ntiles = (p.N + 31) / 32, npairs = (ntiles + 1) / 2;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x / WAVE);
-  int64_t tile = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
-  // X^T fragments (B operand of layer 1): state r, features 16s + 8h .. +7
+  int64_t pair = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
+  // X^T fragments (B operand of layer 1): state r of the tile, features 16s + 8h .. +7
   auto load_x = [&](int64_t tl, bf16x8* xf) {
     const int64_t row = tl * 32 + r;
     const bool ok = tl < ntiles && row < p.N;
     const bf16x8* src = reinterpret_cast<const bf16x8*>(p.x + (ok ? row : 0) * MLP_IN + 8 * h);
 #pragma unroll
-    for (int s = 0; s < MLP_IN / 16; ++s) {
+    for (int s = 0; s < KS1; ++s) {
       const bf16x8 v = src[2 * s];
       xf[s] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
   };
-  bf16x8 xf[MLP_IN / 16], xn[MLP_IN / 16];
-  load_x(tile, xf);
-  for (; tile < ntiles; tile += nw) {
-    load_x(tile + nw, xn);  // next tile in flight during this tile's MFMAs
-    // ---- layer 1: H1^T = relu(W1^T X^T + b1) ----
+  bf16x8 xa[KS1], xb[KS1];
+  load_x(2 * pair, xa);
+  load_x(2 * pair + 1, xb);
+  for (; pair < npairs; pair += nw) {
+    // scheduling fences at the phase boundaries (measured: the scheduler's
+    // cross-phase interleaving is slower than the hand-placed order)
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMPS) {
+      st_last = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- layer 1: H1^T = relu(W1^T X^T + b1), both tiles ----
     // row blocks software-pipelined: block n+1's MFMAs are issued before
     // block n's ReLU/bf16 epilogue, which then runs in their shadow
-    bf16x8 hf[MLP_HID / 16];
-    f32x16 acur = bias_tile(s_b1, h);
+    bf16x8 ha[KS2], hb[KS2];
+    f32x16 ca, cb;
+    {
+      const f32x16 bias = bias_tile(s_b1, h);
+      ca = mfma(w1[0][0], xa[0], bias);
+      cb = mfma(w1[0][0], xb[0], bias);
 #pragma unroll
-    for (int s = 0; s < MLP_IN / 16; ++s) acur = mfma(w1[0][s], xf[s], acur);
-#pragma unroll
-    for (int n = 0; n < MLP_HID / 32; ++n) {
-      f32x16 anext;
-      if (n + 1 < MLP_HID / 32) {
-        anext = bias_tile(s_b1 + 32 * (n + 1), h);
-#pragma unroll
-        for (int s = 0; s < MLP_IN / 16; ++s) anext = mfma(w1[n + 1][s], xf[s], anext);
+      for (int s = 1; s < KS1; ++s) {
+        ca = mfma(w1[0][s], xa[s], ca);
+        cb = mfma(w1[0][s], xb[s], cb);
       }
-      hf[2 * n] = relu_pack(acur, 0);
-      hf[2 * n + 1] = relu_pack(acur, 1);
-      if (n + 1 < MLP_HID / 32) acur = anext;
     }
-    // ---- layer 2: H2^T = relu(W2^T H1^T + b2) ----
-    f32x16 a2[MLP_HID / 32];
 #pragma unroll
-    for (int n = 0; n < MLP_HID / 32; ++n) a2[n] = bias_tile(s_b2 + 32 * n, h);
-    // W2 fragments software-pipelined one k-step ahead (LDS latency hidden
-    // behind the current k-step's 8 MFMAs); the barriers keep exactly two
-    // k-steps of fragments in registers (the scheduler would otherwise hoist
-    // all 128 fragment reads and spill)
-    bf16x8 wf[MLP_HID / 32], wn[MLP_HID / 32];
+    for (int n = 0; n < NB; ++n) {
+      f32x16 na, nb;
+      if (n + 1 < NB) {
+        const f32x16 bias = bias_tile(s_b1 + 32 * (n + 1), h);
+        na = mfma(w1[n + 1][0], xa[0], bias);
+        nb = mfma(w1[n + 1][0], xb[0], bias);
 #pragma unroll
-    for (int n = 0; n < MLP_HID / 32; ++n) wf[n] = s_w2[n * (MLP_HID / 16) * WAVE + lane];
-#pragma unroll
-    for (int kk = 0; kk < MLP_HID / 16; ++kk) {
-      if (kk + 1 < MLP_HID / 16) {
-#pragma unroll
-        for (int n = 0; n < MLP_HID / 32; ++n) wn[n] = s_w2[(n * (MLP_HID / 16) + kk + 1) * WAVE + lane];
+        for (int s = 1; s < KS1; ++s) {
+          na = mfma(w1[n + 1][s], xa[s], na);
+          nb = mfma(w1[n + 1][s], xb[s], nb);
+        }
       }
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int n = 0; n < MLP_HID / 32; ++n) a2[n] = mfma(wf[n], hf[kk], a2[n]);
-#pragma unroll
-      for (int n = 0; n < MLP_HID / 32; ++n) wf[n] = wn[n];
+      ha[2 * n] = relu_pack(ca, 0);
+      ha[2 * n + 1] = relu_pack(ca, 1);
+      hb[2 * n] = relu_pack(cb, 0);
+      hb[2 * n + 1] = relu_pack(cb, 1);
+      if (n + 1 < NB) { ca = na; cb = nb; }
     }
-    // ---- layer 3: Y^T = W3^T H2^T + b3 (rows 8..31 of W3^T are zero) ----
-    // interleaved with layer 2's epilogue: k-steps 2n, 2n+1 need only block n
-    f32x16 a3 = bias_tile(s_b3, h);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMPS) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st[0] += now - st_last;
+      st_last = now;
+    }
+    // next pair's states in flight during layers 2 and 3
+    load_x(2 * (pair + nw), xa);
+    load_x(2 * (pair + nw) + 1, xb);
+    // ---- layers 2 and 3: one 32-row block of H2 at a time, software-
+    // pipelined: while block m+1's 16 k-steps run (2 MFMAs each, one W2
+    // fragment read two k-steps ahead), block m's ReLU/bf16 epilogue and its
+    // two layer-3 k-steps are spread over those k-steps ----
+    f32x16 ya = bias_tile(s_b3, h), yb = ya;
+    auto w2 = [&](int m, int kk) { return s_w2[(m * KS2 + kk) * WAVE + lane]; };
+    {
+      bf16x8 w0 = w2(0, 0), w1f = w2(0, 1);
+      const f32x16 bias = bias_tile(s_b2, h);
 #pragma unroll
-    for (int n = 0; n < MLP_HID / 32; ++n) {
-      const bf16x8 g0 = relu_pack(a2[n], 0), g1 = relu_pack(a2[n], 1);
-      a3 = mfma(s_w3[(2 * n) * WAVE + lane], g0, a3);
-      a3 = mfma(s_w3[(2 * n + 1) * WAVE + lane], g1, a3);
+      for (int kk = 0; kk < KS2; ++kk) {
+        const bf16x8 wn = kk + 2 < KS2 ? w2(0, kk + 2) : w2(1, kk + 2 - KS2);
+        asm volatile("" ::: "memory");
+        ca = kk == 0 ? mfma(w0, ha[0], bias) : mfma(w0, ha[kk], ca);
+        cb = kk == 0 ? mfma(w0, hb[0], bias) : mfma(w0, hb[kk], cb);
+        w0 = w1f;
+        w1f = wn;
+      }
+#pragma unroll
+      for (int m = 0; m < NB; ++m) {
+        f32x16 na, nb;
+        bf16x8 ga0, ga1, gb0, gb1, w30, w31;
+        if (m + 1 < NB) {
+          const f32x16 bn = bias_tile(s_b2 + 32 * (m + 1), h);
+#pragma unroll
+          for (int kk = 0; kk < KS2; ++kk) {
+            const int q = (m + 1) * KS2 + kk + 2;  // fragment two k-steps ahead (wraps into the next block)
+            const bf16x8 wn = q < NB * KS2 ? s_w2[q * WAVE + lane] : w0;
+            asm volatile("" ::: "memory");
+            na = kk == 0 ? mfma(w0, ha[0], bn) : mfma(w0, ha[kk], na);
+            nb = kk == 0 ? mfma(w0, hb[0], bn) : mfma(w0, hb[kk], nb);
+            w0 = w1f;
+            w1f = wn;
+            if (kk == 1) ga0 = relu_pack(ca, 0);
+            if (kk == 3) ga1 = relu_pack(ca, 1);
+            if (kk == 5) gb0 = relu_pack(cb, 0);
+            if (kk == 7) gb1 = relu_pack(cb, 1);
+            if (kk == 7) { w30 = s_w3[(2 * m) * WAVE + lane]; w31 = s_w3[(2 * m + 1) * WAVE + lane]; }
+            if (kk == 9) ya = mfma(w30, ga0, ya);
+            if (kk == 11) yb = mfma(w30, gb0, yb);
+            if (kk == 13) ya = mfma(w31, ga1, ya);
+            if (kk == 15) yb = mfma(w31, gb1, yb);
+          }
+          ca = na;
+          cb = nb;
+        } else {
+          w30 = s_w3[(2 * m) * WAVE + lane];
+          w31 = s_w3[(2 * m + 1) * WAVE + lane];
+          ya = mfma(w30, relu_pack(ca, 0), ya);
+          yb = mfma(w30, relu_pack(cb, 0), yb);
+          ya = mfma(w31, relu_pack(ca, 1), ya);
+          yb = mfma(w31, relu_pack(cb, 1), yb);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMPS) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      st[1] += now - st_last;
     }
     // registers 0..3 hold outputs 4h..4h+3 of state r
-    const int64_t row = tile * 32 + r;
-    if (row < p.N) *reinterpret_cast<f32x4*>(p.y + row * MLP_OUT + 4 * h) = f32x4{a3[0], a3[1], a3[2], a3[3]};
-#pragma unroll
-    for (int s = 0; s < MLP_IN / 16; ++s) xf[s] = xn[s];
+    const int64_t ra = (2 * pair) * 32 + r, rb = ra + 32;
+    if (ra < p.N) *reinterpret_cast<f32x4*>(p.y + ra * MLP_OUT + 4 * h) = f32x4{ya[0], ya[1], ya[2], ya[3]};
+    if (rb < p.N) *reinterpret_cast<f32x4*>(p.y + rb * MLP_OUT + 4 * h) = f32x4{yb[0], yb[1], yb[2], yb[3]};
+  }
+  if constexpr (STAMPS) {
+    if (lane == 0) {
+      atomicAdd(&p.stamps[0], st[0]);
+      atomicAdd(&p.stamps[1], st[1]);
+      // whole-wave shader cycles and 100 MHz real-time ticks: the clock the kernel ran at
+      atomicAdd(&p.stamps[2], __builtin_amdgcn_s_memtime() - k0);
+      atomicAdd(&p.stamps[3], __builtin_amdgcn_s_memrealtime() - r0);
+    }
   }
 }
 
@@ -195,7 +283,8 @@ __global__ void __launch_bounds__(256) mlp_gen_states_kernel(uint16_t* x, int64_
 }
 
 hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s) {
-  hipLaunchKernelGGL(mlp_kernel, dim3((unsigned)cus), dim3(256), 0, s, p);
+  if (p.stamps) hipLaunchKernelGGL(mlp_kernel<true>, dim3((unsigned)cus), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(mlp_kernel<false>, dim3((unsigned)cus), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
