@@ -150,7 +150,8 @@ static int dupload(ccka_ctx* c, T*& dst, const T* src, size_t count) {
 // Single-deployment engine: eligibility and world digest.
 // Conditions (anything else runs the general kernel): one HPA Deployment, no
 // NodePool CPU limits (the launch choice is then independent of pool usage),
-// replica counts and records within int16, tolerance in [0, 1), at most
+// replica counts and records within int16, tolerance in [0, 1), PDB percent
+// <= 100, at most 65535 steps, at most
 // D1_MAX_ZI distinct zone masks and D1_MAX_WC distinct carbon weights.
 // ---------------------------------------------------------------------------
 static int pod_cap(const ccka_itype& t, int rc, int rm) {
@@ -198,6 +199,8 @@ static int d1_check_world(ccka_ctx* c) {
   if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
       dp.min_replicas < 0 || dp.max_replicas < 0 || dp.max_replicas > D1_REC_SAT || dp.replicas0 > D1_REC_SAT)
     return CCKA_OK;
+  // 32-bit PDB arithmetic (pct x replicas) and pending-pod-minutes (pods x steps)
+  if (w.pdb_min_available_pct > 100 || w.n_steps > 65535) return CCKA_OK;
   const int K = w.n_types;
   std::vector<int> cap1(K);
   int jmax = 0;

@@ -385,7 +385,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   bool dirty = true;
   int wake = 0;
   int profile = -1, hour = -1;
-  long long cost = 0, pend_min = 0, burn = 0, base_price = 0;
+  long long cost = 0, burn = 0, base_price = 0;
+  int pend_min = 0;  // <= 32767 pods x T steps
   // energy in exact nanowatt-minutes. Cached over the slots (refreshed when a
   // slot's pods, readiness or existence changed): I = sum of idle draw,
   // S = sum over ready slots of dyn_nw_per_m * pods, R = max over ready slots
@@ -696,21 +697,21 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       uint32_t elig = eb[0];
       const uint32_t empty_m = mb[0];
       const int F = fv[0];
-      int wk = wv[0];
-      long long allowed = 0x3fffffffffffffffLL;
+      int wk = opqv(wv[0]);  // materialise now (the compiler would otherwise keep 8 compare masks alive)
+      // PDB evictions allowed (32-bit: pct <= 100 and replicas <= 32767)
+      int allowed = 0x7fffffff;
       if (pdb_pct >= 0) {
-        const long long rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
-        allowed = max(rdyp - ((long long)pdb_pct * reps + 99) / 100, 0LL);
+        const int rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
+        allowed = max(rdyp - (int)(((uint32_t)(pdb_pct * reps) + 99u) / 100u), 0);
       }
       // WhenEmptyOrUnderutilized test of every slot (SEMANTICS §3.G): its pods
       // fit on the other compatible ready slots (F minus its own free space)
       // and the PDB allows evicting them
       uint32_t ub[MAXN];
-      const int allowed32 = (int)min(allowed, 0x7fffffffLL);
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
         const int need = (cmask >> n & 1u) ? scap[n] : spods[n];
-        ub[n] = (need <= F && (!pdb_member || spods[n] <= allowed32)) ? (1u << n) : 0u;
+        ub[n] = (need <= F && (!pdb_member || spods[n] <= allowed)) ? (1u << n) : 0u;
       }
 #pragma unroll
       for (int w = MAXN / 2; w > 0; w >>= 1)
@@ -747,7 +748,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               bool ok = pods == 0;
               if (!ok && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) {
                 const int fo = F - ((cmask >> n & 1u) ? scap[n] - pods : 0);
-                ok = fo >= pods && (!pdb_member || (long long)pods <= allowed);
+                ok = fo >= pods && (!pdb_member || pods <= allowed);
               }
               const unsigned long long key = (unsigned long long)pods << 36 |
                                              (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
@@ -834,7 +835,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
     long long e_step;
     if ((float)upp * Rmax < 0.9999f && !(ablate & 4)) {
-      e_step = base_nw + Isum + (long long)upp * Ssum;
+      e_step = base_nw + Isum + (long long)((unsigned long long)(uint32_t)upp * (unsigned long long)Ssum);
     } else {  // a node saturates (use clamped at its allocatable CPU)
       e_step = base_nw + Isum;
 #pragma unroll

@@ -23,9 +23,12 @@ for mask in (16, 16 | 1):
     buf = (C.c_ulonglong * 12)()
     assert eng.lib.ccka_debug_stamps(eng.ctx, buf) == 0
     tot = sum(buf)
-    waves = (100_000 + 63) // 64
+    lpw = min(64, max(32, -(-100_000 // (2 * 4 * 256))))  # the engine's automatic lanes per wave
+    waves = -(-100_000 // lpw)
     print(f"mask {mask}: kernel {eng.kernel_ms():.3f} ms; cycles per wave-step by phase:")
     tot = sum(list(buf)[:10])
     for n, v in zip(names, list(buf)[:10]):
         print(f"  {n:22s} {v / waves / 1440:9.1f}  {100.0 * v / tot:5.1f} %")
+    print(f"  shader clock ~ {sum(list(buf)[:10]) / waves / (eng.kernel_ms() * 1e-3) / 1e9:.2f} GHz "
+          f"(stamped cycles per wave / kernel time)")
     print(f"  wave-steps evaluating disruption {buf[10] / waves / 1440:.3f}, running HPA behavior {buf[11] / waves / 1440:.3f}")
