@@ -214,12 +214,19 @@ def main():
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},
+            # the kernel is issue-bound, not HBM-bound: its measured issue-side
+            # utilisation (profiled) and the measured copy ceiling
+            "issue": profiled_issue(cfg),
             "totals": {"cost_usd": totals.cost_uphmin / 6e7, "energy_kwh": totals.energy_wmin / 6e4,
                        "gco2_kg": totals.gco2 / 1e3, "slo_minutes": totals.slo_minutes,
                        "launches": totals.launches, "deletions": totals.deletions},
         }
         if cfg == 4:
             out["pareto_frontier_grids"] = frontier[-1] if frontier else None
+        if rank == 0:
+            cbw = copy_bandwidth()
+            out["roofline"]["copy_gbs"] = cbw
+            out["roofline"]["frac_of_copy"] = achieved / cbw
         if rank == 0 and world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(eng, spec, sc, args.cpu_seconds)
     if rank == 0:
@@ -242,6 +249,44 @@ def measured_traffic(cfg, traj, n, T):
     if not paths:
         return None
     return json.load(open(paths[-1])).get("traffic_bytes")
+
+
+def copy_bandwidth(nbytes=1 << 31, reps=5):
+    """Measured device copy rate (GB/s of read + write) of a plain 2 GiB
+    device-to-device copy on this GPU, the practical HBM ceiling the rollout's
+    achieved bytes are also compared against."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
+def profiled_issue(cfg):
+    """Issue-side utilisation of the rollout kernel for this config from the
+    committed rocprofv3 PMC pass (tools/prof_issue.sh -> profiles/round*/
+    issue_config234.json): VALU / SALU issue fractions of SIMD cycles, mean
+    active lanes per VALU instruction, clock. None when no profile exists."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*", "issue_config234.json")))
+    if not paths:
+        return None
+    d = json.load(open(paths[-1])).get(f"config{cfg}")
+    if d:
+        d = dict(d, source=os.path.relpath(paths[-1], ROOT))
+    return d
 
 
 def cpu_baseline(eng, spec, sc, target_s):
