@@ -188,6 +188,16 @@ static D1Rule d1_rule(const ccka_hpa_rules& r, bool up) {
   return o;
 }
 
+// the rules as the kernel uses them equal the upstream default behavior
+// (d1_default_rule; the down stabilisation window is per scenario, not here)
+static bool d1_rule_is_default(const D1Rule& r, bool up) {
+  const D1Rule d = d1_default_rule(up);
+  if (r.sel != d.sel || r.n != d.n || (up && r.stab_mask != 0)) return false;
+  for (int q = 0; q < r.n; ++q)
+    if (r.type[q] != d.type[q] || r.value[q] != d.value[q] || r.pmask[q] != 0) return false;
+  return true;
+}
+
 static int d1_check_world(ccka_ctx* c) {
   const ccka_world& w = c->hw;
   c->d1_world = false;
@@ -270,6 +280,7 @@ static int d1_check_world(ccka_ctx* c) {
               (bt.idle_nw + bt.dyn_nw_per_m * (long long)(w.base_util * (double)bt.alloc_cpu_m));
   p.up = d1_rule(dp.up, true);
   p.dn = d1_rule(dp.down, false);
+  p.bdef = d1_rule_is_default(p.up, true) && d1_rule_is_default(p.dn, false);
   c->d1_world = true;
   return CCKA_OK;
 }
@@ -1127,9 +1138,9 @@ int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
   return CCKA_OK;
 }
 
-// Internal: occupancy target of the single-deployment kernel (2, 3, 4; 0 = automatic).
+// Internal: occupancy target of the single-deployment kernel (2, 3; 0 = automatic).
 int ccka_debug_occ(ccka_ctx* c, int32_t occ) {
-  if (!c || occ < 0 || occ > 4 || occ == 1) return CCKA_EINVAL;
+  if (!c || occ < 0 || occ > 3 || occ == 1) return CCKA_EINVAL;
   c->occ = occ;
   return CCKA_OK;
 }

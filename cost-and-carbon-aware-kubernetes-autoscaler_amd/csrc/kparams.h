@@ -109,6 +109,26 @@ struct D1Rule {
   int32_t pm16[2][4];
 };
 
+// Upstream default HPA behavior (autoscaling/v2 defaults): scale-up
+// max(Percent 100, Pods 4) per 15 s without stabilisation, scale-down
+// Percent 100 per 15 s (its window is per scenario). 15 s periods hold no
+// 60 s history entry, so pmask = 0. The single-deployment kernel has an
+// instantiation with these rules as compile-time constants (no rule registers).
+constexpr D1Rule d1_default_rule(bool up) {
+  D1Rule r{};
+  r.sel = CCKA_SELECT_MAX;
+  r.n = up ? 2 : 1;
+  r.type[0] = CCKA_HPA_PERCENT;
+  r.value[0] = 100;
+  r.factor[0] = up ? 1.0 + 100.0 / 100.0 : 1.0 - 100.0 / 100.0;
+  if (up) {
+    r.type[1] = CCKA_HPA_PODS;
+    r.value[1] = 4;
+    r.factor[1] = 1.0 + 4.0 / 100.0;
+  }
+  return r;
+}
+
 // one profile patch of one pool, pre-digested: policy 0 / cas -1 / zi -1 / cm 0 = keep
 struct D1Patch {
   int32_t policy, cas, zi, cm;  // cas = ceil(consolidate_after_s / 60) steps
@@ -149,7 +169,8 @@ struct D1Params {
   int64_t N;
   int64_t NL, trace_mod, first_id;  // load columns / shared-trace mapping (as KParams)
   int32_t lpw;  // scenarios per wave (<= 64; fewer lanes = less divergence per wave)
-  int32_t occ;  // register-allocation occupancy target of the instantiation (2, 3 or 4)
+  int32_t occ;   // register-allocation occupancy target of the instantiation (2 or 3)
+  int32_t bdef;  // 1: up/dn are the upstream default behavior (d1_default_rule)
   int32_t T, K, Z, R, NP, maxn, NZI, NW, JT;
   int32_t start_minute, peak_start, peak_end, pswitch0, delay;
   int32_t base_nodes, base_type, slo_util, pdb_pct, pdb_member;

@@ -272,7 +272,7 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
     st_last = now_;                                          \
   }
 
-template <int MAXN, int MAXP, bool STAMPS, int OCC>
+template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -319,7 +319,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const GLOBAL_AS int2* const table = opq_ptr(p.table);
   const GLOBAL_AS int32_t* const jtab = opq_ptr(p.jtab);
   GLOBAL_AS int4* const traj = opq_ptr(reinterpret_cast<int4*>(p.traj));
-  const D1Rule rup = opq_rule(p.up), rdn = opq_rule(p.dn);
+  // BDEF: the upstream default behavior as compile-time constants
+  const D1Rule rup = [&] { if constexpr (BDEF) return d1_default_rule(true); else return opq_rule(p.up); }();
+  const D1Rule rdn = [&] { if constexpr (BDEF) return d1_default_rule(false); else return opq_rule(p.dn); }();
   int budget[MAXP];
 #pragma unroll
   for (int q = 0; q < MAXP; ++q) budget[q] = opq(p.budget[q]);
@@ -896,22 +898,23 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const unsigned grid = (unsigned)((waves + B / WAVE - 1) / (B / WAVE));
   const size_t lds = (size_t)p.K * sizeof(int4);
   // OCC = resident waves per SIMD the register allocation targets: 2 (no
-  // spills) when the batch is a single round of waves, 3 for multi-round
-  // batches (configs 3/4), where more resident waves hide more latency
-  if (p.stamps)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2>), dim3(grid), dim3(B), lds, s, p);
-  else if (p.maxn <= 8 && p.NP <= 2 && p.occ >= 4)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 4>), dim3(grid), dim3(B), lds, s, p);
-  else if (p.maxn <= 8 && p.NP <= 2 && p.occ == 3)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 3>), dim3(grid), dim3(B), lds, s, p);
-  else if (p.maxn <= 8 && p.NP <= 2)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2>), dim3(grid), dim3(B), lds, s, p);
-  else if (p.maxn <= 8)
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false, 2>), dim3(grid), dim3(B), lds, s, p);
-  else if (p.NP <= 2)
-    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false, 1>), dim3(grid), dim3(B), lds, s, p);
-  else
-    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false, 1>), dim3(grid), dim3(B), lds, s, p);
+  // spills); 3 is a diagnostic instantiation (spills, measured slower)
+  const bool d = p.bdef != 0;
+  if (p.stamps) {
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, p);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, false>), dim3(grid), dim3(B), lds, s, p);
+  } else if (p.maxn <= 8 && p.NP <= 2 && p.occ == 3) {
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 3, false>), dim3(grid), dim3(B), lds, s, p);
+  } else if (p.maxn <= 8 && p.NP <= 2) {
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true>), dim3(grid), dim3(B), lds, s, p);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false>), dim3(grid), dim3(B), lds, s, p);
+  } else if (p.maxn <= 8) {
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false, 2, false>), dim3(grid), dim3(B), lds, s, p);
+  } else if (p.NP <= 2) {
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false, 1, false>), dim3(grid), dim3(B), lds, s, p);
+  } else {
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false, 1, false>), dim3(grid), dim3(B), lds, s, p);
+  }
   return hipGetLastError();
 }
 

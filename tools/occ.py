@@ -14,7 +14,7 @@ eng.lib.ccka_debug_occ.argtypes = [C.c_void_p, C.c_int32]
 eng.lib.ccka_debug_lpw.argtypes = [C.c_void_p, C.c_int32]
 # config 2 is one resident round at 2 waves/SIMD: refill the round for the
 # occupancy being tested (lanes per wave = N / (occ * 4 SIMDs * CUs))
-LPW2 = {2: 0, 3: 33, 4: 25}
+LPW2 = {2: 0, 3: 33}
 cases = {
     "config2": (configs.config2_world(), configs.hpa_scenarios(100_000), configs.trace_gen(), True),
     "config3": (configs.config3_world(), configs.config3_scenarios(1_000_000), configs.trace_gen(), False),
@@ -27,7 +27,7 @@ for name, (spec, sc, gen, traj) in cases.items():
     ref = None
     res = {}
     for r in range(2):
-        for occ in (2, 3, 4):
+        for occ in (2, 3):
             eng.lib.ccka_debug_occ(eng.ctx, occ)
             eng.lib.ccka_debug_lpw(eng.ctx, LPW2[occ] if name == "config2" else 0)
             eng.rollout(trajectory=traj)
