@@ -345,7 +345,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   }
 
   // consolidateAfter (steps) of a slot's pool: explicit selects on the pool
-  // bits (an indexed pcas[] would be demoted to scratch memory)
+  // bits (an indexed pcas[] would be demoted to scratch memory). Each slot
+  // carries its pool's value in sinfo bits 16..31 (clamped to 0xFFFF: with
+  // T <= 65535 a larger value never makes a node consolidatable either), so
+  // the per-touch update is one shift; this select runs only when a pool's
+  // value changes (profile switch) or a slot is created.
   auto cas_of = [&](uint32_t info) {
     const int m1 = -(int)(info >> 13 & 1u), m2 = -(int)(info >> 14 & 1u);
     const int lo = pcas[0] ^ ((pcas[0] ^ pcas[MAXP > 1 ? 1 : 0]) & m1);
@@ -358,7 +362,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   };
 
   // ---- node slots (register arrays, fully unrolled loops) ----
-  uint32_t sinfo[MAXN];  // type | zone<<10 | cap<<12 | pool<<13
+  uint32_t sinfo[MAXN];  // type | zone<<10 | cap<<12 | pool<<13 | consolidateAfter steps<<16
+  auto cas16 = [](int c) { return (uint32_t)min(c, 0xFFFF) << 16; };
   int sready[MAXN], slast[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN], selig[MAXN];
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
   float sinvf[MAXN];    // 1/alloc (saturation pre-test only; the energy itself is exact)
@@ -488,7 +493,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       // consolidateAfter may have changed: per-slot copies and thresholds
 #pragma unroll
       for (int n = 0; n < MAXN; ++n)
-        if (used >> n & 1u) selig[n] = max(sready[n], slast[n] + cas_of(sinfo[n]));
+        if (used >> n & 1u) {
+          sinfo[n] = (sinfo[n] & 0xFFFFu) | cas16(cas_of(sinfo[n]));
+          selig[n] = max(sready[n], slast[n] + (int)(sinfo[n] >> 16));
+        }
       refresh_J(rh);
     }
 
@@ -574,17 +582,19 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
+        int removed = 0;
 #pragma unroll
-        for (int n = MAXN - 1; n >= 0; --n) {
-          if ((m >> n & 1u) && spods[n] > 0 && excess > 0) {
-            const int k = min(spods[n], excess);
-            spods[n] -= k;
-            excess -= k;
+        for (int n = MAXN - 1; n >= 0; --n) {  // branch-free: k = 0 leaves the slot untouched
+          const int k = (m >> n & 1u) ? min(spods[n], excess) : 0;
+          spods[n] -= k;
+          excess -= k;
+          removed += k;
+          if (k > 0) {  // if-converted selects
             slast[n] = t;
-            selig[n] = max(sready[n], t + cas_of(sinfo[n]));
-            if (pass == 1) rpods -= k;
+            selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
           }
         }
+        if (pass == 1) rpods -= removed;
       }
     }
     // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
@@ -593,20 +603,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask;
+        int added = 0;
 #pragma unroll
-        for (int n = 0; n < MAXN; ++n) {
-          if (pd > 0 && (m >> n & 1u)) {
-            const int k = min(scap[n] - spods[n], pd);
-            if (k > 0) {
-              spods[n] += k;
-              pd -= k;
-              placed += k;
-              slast[n] = t;
-              selig[n] = max(sready[n], t + cas_of(sinfo[n]));
-              if (pass == 0) { rpods += k; dirty = true; acc_dirty = true; }
-            }
+        for (int n = 0; n < MAXN; ++n) {  // branch-free first fit
+          const int k = (m >> n & 1u) ? max(min(scap[n] - spods[n], pd), 0) : 0;
+          spods[n] += k;
+          pd -= k;
+          added += k;
+          if (k > 0) {  // if-converted selects
+            slast[n] = t;
+            selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
           }
         }
+        placed += added;
+        if (pass == 0 && added > 0) { rpods += added; dirty = true; acc_dirty = true; }
       }
     }
     D1_STAMP(3);
@@ -636,7 +646,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
               if (n == slot) {
-                sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13);
+                sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13) | cas16(cq);
                 sready[n] = rs;
                 slast[n] = t;
                 spods[n] = k;
@@ -769,7 +779,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                   spods[n] += k;
                   need -= k;
                   slast[n] = t;
-                  selig[n] = max(sready[n], t + cas_of(sinfo[n]));
+                  selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
                 }
               }
             }
