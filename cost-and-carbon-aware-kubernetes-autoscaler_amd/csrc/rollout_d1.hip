@@ -367,10 +367,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int sready[MAXN], slast[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN], selig[MAXN];
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
   float sinvf[MAXN];    // 1/alloc (saturation pre-test only; the energy itself is exact)
+  int salloc[MAXN];     // alloc_cpu_m of the slot's type (< 2^24 by eligibility)
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
     sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0; selig[n] = 0;
-    sdyn[n] = 0; sinvf[n] = 0.f;
+    sdyn[n] = 0; sinvf[n] = 0.f; salloc[n] = 0;
 
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
@@ -655,6 +656,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 selig[n] = el;
                 sdyn[n] = (uint32_t)ac.z;
                 sinvf[n] = __builtin_amdgcn_rcpf((float)ac.w);
+                salloc[n] = ac.w;
               }
             }
             const uint32_t bit = 1u << slot;
@@ -793,6 +795,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
                 sdyn[n] = 0;
                 sinvf[n] = 0.f;
+                salloc[n] = 0;
                 sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
                 selig[n] = 0;
               }
@@ -848,14 +851,17 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     long long e_step;
     if ((float)upp * Rmax < 0.9999f && !(ablate & 4)) {
       e_step = base_nw + Isum + (long long)((unsigned long long)(uint32_t)upp * (unsigned long long)Ssum);
-    } else {  // a node saturates (use clamped at its allocatable CPU)
+    } else {  // a node saturates (use clamped at its allocatable CPU): branch-free,
+              // 24-bit products (pods < 2^15, clamped upp < 2^24, alloc < 2^24)
       e_step = base_nw + Isum;
+      const uint32_t uc = (uint32_t)min(upp, 0xFFFFFF);
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        if (!(rdy >> n & 1u)) continue;
-        const int4 a = s_acc[sinfo[n] & 1023u];
-        const long long use = min((long long)spods[n] * upp, (long long)a.w);
-        e_step += (long long)(unsigned)a.z * use;
+        const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] & 0x7FFFu : 0u;
+        const uint64_t prod = (uint64_t)pr * (uint64_t)uc;
+        const uint32_t al = (uint32_t)salloc[n] & 0xFFFFFFu;
+        const uint32_t use = prod < (uint64_t)al ? (uint32_t)prod : al;
+        e_step += (long long)((uint64_t)sdyn[n] * use);
       }
     }
     cost += burn + base_price;
