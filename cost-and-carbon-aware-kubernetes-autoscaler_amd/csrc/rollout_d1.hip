@@ -390,6 +390,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     dn16[w] = ((dnmask >> (2 * w)) & 1 ? 0xFFFFu : 0u) | ((dnmask >> (2 * w + 1)) & 1 ? 0xFFFF0000u : 0u);
   }
   int next_ready = 0x7fffffff, nsp = 0, nod = 0;
+  // free pod capacity of the compatible ready slots (kept incrementally:
+  // readiness, reconcile of running pods, scheduling onto ready slots,
+  // zero-delay launches; recomputed after a deletion)
+  int Ffree = 0;
   bool dirty = true;
   int wake = 0;
   int profile = -1, hour = -1;
@@ -468,7 +472,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
         if ((used & ~rdy) >> n & 1u) {
-          if (sready[n] <= t) { rdy |= 1u << n; rpods += spods[n]; acc_dirty = true; }
+          if (sready[n] <= t) {
+            rdy |= 1u << n;
+            rpods += spods[n];
+            acc_dirty = true;
+            if (cmask >> n & 1u) Ffree += scap[n] - spods[n];
+          }
           else next_ready = min(next_ready, sready[n]);
         }
       }
@@ -570,7 +579,13 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       ring_push(hup, ran ? rv : 0x7FFF);
     }
     ring_push(hdel, (hpa_path && desired != cur) ? desired - cur : 0);
-    if (desired != cur) dirty = true;
+    // Disruption is re-evaluated after a scale-DOWN only. A scale-up leaves
+    // every ready slot as it was unless pods land on one (scheduling pass 0
+    // marks that), lowers the PDB allowance (fewer candidates) and adds only
+    // in-flight slots or in-flight pods (readiness marks those), so an
+    // evaluation that found no deletion finds none again; a scale-down can
+    // raise the PDB allowance without moving a pod.
+    if (desired < cur) dirty = true;
     replicas = desired;
 
     D1_STAMP(2);
@@ -583,19 +598,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
-        int removed = 0;
+        int removed = 0, removed_c = 0;
 #pragma unroll
         for (int n = MAXN - 1; n >= 0; --n) {  // branch-free: k = 0 leaves the slot untouched
           const int k = (m >> n & 1u) ? min(spods[n], excess) : 0;
           spods[n] -= k;
           excess -= k;
           removed += k;
+          if (pass == 1) removed_c += (cmask >> n & 1u) ? k : 0;
           if (k > 0) {  // if-converted selects
             slast[n] = t;
             selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
           }
         }
-        if (pass == 1) rpods -= removed;
+        if (pass == 1) { rpods -= removed; Ffree += removed_c; }
       }
     }
     // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
@@ -617,7 +633,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           }
         }
         placed += added;
-        if (pass == 0 && added > 0) { rpods += added; dirty = true; acc_dirty = true; }
+        if (pass == 0 && added > 0) { rpods += added; Ffree -= added; dirty = true; acc_dirty = true; }
       }
     }
     D1_STAMP(3);
@@ -667,7 +683,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             placed += k;
             acc_dirty = true;
             Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
-            if (delay == 0) { rdy |= bit; rpods += k; dirty = true; }
+            if (delay == 0) {
+              rdy |= bit;
+              rpods += k;
+              dirty = true;
+              if (cmask & bit) Ffree += cap1 - k;
+            }
             else next_ready = min(next_ready, rs);
             if (bc == 0) nsp++; else nod++;
             burn += price;
@@ -691,12 +712,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       // slots, empty slots, the free capacity F of the compatible ready slots
       // and the next wake-up step.
       uint32_t eb[MAXN], mb[MAXN];
-      int fv[MAXN], wv[MAXN];
+      int wv[MAXN];
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {  // independent per-slot terms, then pairwise trees
         eb[n] = ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
         mb[n] = spods[n] == 0 ? (1u << n) : 0u;
-        fv[n] = ((rdy & cmask) >> n & 1u) ? scap[n] - spods[n] : 0;
         wv[n] = ((used >> n & 1u) && selig[n] > t) ? selig[n] : 0x7fffffff;
       }
 #pragma unroll
@@ -705,12 +725,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         for (int n = 0; n < w; ++n) {
           eb[n] |= eb[n + w];
           mb[n] |= mb[n + w];
-          fv[n] += fv[n + w];
           wv[n] = min(wv[n], wv[n + w]);
         }
       uint32_t elig = eb[0];
       const uint32_t empty_m = mb[0];
-      const int F = fv[0];
+      const int F = Ffree;
       int wk = opqv(wv[0]);  // materialise now (the compiler would otherwise keep 8 compare masks alive)
       // PDB evictions allowed (32-bit: pct <= 100 and replicas <= 32767)
       int allowed = 0x7fffffff;
@@ -737,7 +756,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       for (int q = 0; q < MAXP; ++q) {
         if (q >= NP) break;
         valid |= elig & pmask[q] & (empty_m | (ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED ? under_m : 0u));
-        if (pmask[q] && (budget[q] * __popc(pmask[q]) + 99) / 100 <= 0) budget_hit = true;
+        // ceil(budget% x nodes) <= 0 with nodes > 0  <=>  budget% <= 0
+        if (pmask[q] && budget[q] <= 0) budget_hit = true;
       }
       if (valid) {  // exact sequential evaluation (a deletion happens this step)
 #pragma unroll
@@ -815,7 +835,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         }
       }
       dirty = budget_hit || any_del;
-      if (any_del) {  // slots changed: next step at which a node becomes consolidatable
+      if (any_del) {
+        Ffree = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) Ffree += ((rdy & cmask) >> n & 1u) ? scap[n] - spods[n] : 0;  // slots changed: next step at which a node becomes consolidatable
         wk = 0x7fffffff;
 #pragma unroll
         for (int n = 0; n < MAXN; ++n) if ((used >> n & 1u) && selig[n] > t) wk = min(wk, selig[n]);
