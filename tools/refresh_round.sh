@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# Every measurement committed under profiles/<round>/, in one GPU call:
+# bench lines of configs 2-5 (with the CPU baselines), the config-2 kernel
+# trace + HBM + SQ counters and the config-5 trace + MFMA counters
+# (prof_round1.sh), issue-side counters of configs 2-4 (prof_issue.sh) and
+# the MLP SQ counters (prof_mlp.sh). Output: gpurun_out/refresh/.
+# usage: tools/refresh_round.sh
+out=gpurun_out/refresh
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p $out
+for c in 2 3 4 5; do
+  tools/gpu_step.sh bench_full_c$c 400 python bench.py --config $c || exit $?
+  grep '^{' gpurun_out/bench_full_c$c.log | tail -1 > $out/bench_config$c.json || exit 1
+done
+tools/prof_round1.sh $out/p1 || exit $?
+tools/prof_issue.sh $out/issue || exit $?
+tools/prof_mlp.sh $out/mlp || exit $?
+echo refresh-done
