@@ -593,7 +593,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     if (placed > replicas) {
       int excess = placed - replicas;
       dirty = true;
-      acc_dirty = true;
       placed = replicas;
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
@@ -611,7 +610,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
           }
         }
-        if (pass == 1) { rpods -= removed; Ffree += removed_c; }
+        // the cached energy sums cover ready slots only: pass 1 refreshes them
+        if (pass == 1) { rpods -= removed; Ffree += removed_c; acc_dirty = acc_dirty || removed > 0; }
       }
     }
     // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
@@ -681,12 +681,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
             for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
             placed += k;
-            acc_dirty = true;
-            Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
+            Isum += ((long long)ac.y << 32) | (unsigned)ac.x;  // idle draw from launch on
             if (delay == 0) {
               rdy |= bit;
               rpods += k;
               dirty = true;
+              acc_dirty = true;
               if (cmask & bit) Ffree += cap1 - k;
             }
             else next_ready = min(next_ready, rs);
