@@ -21,11 +21,13 @@ def torch_ref(x_bits, ws_bits, bs):
     return (h2 @ w3 + b3).numpy()
 
 
-def test_mlp_exact_integer_data(engine):
+@pytest.mark.parametrize("n", [32 * 37 + 5, 32 * 38 + 7, 64 * 256 * 4 + 33, 31, 1])
+def test_mlp_exact_integer_data(engine, n):
     """Small integers: every product, sum and bf16 activation is exact, so any
-    fragment-layout / k-order error shows up as an exact mismatch."""
+    fragment-layout / k-order error shows up as an exact mismatch. Sizes: a
+    ragged last tile, an odd number of tiles (a wave's pair half empty), more
+    tiles than resident waves, and single-tile batches."""
     rng = np.random.default_rng(3)
-    n = 32 * 37 + 5  # ragged last tile
     x = rng.integers(-1, 2, size=(n, 64)).astype(np.float32)
     w1 = rng.integers(-1, 2, size=(64, 256)).astype(np.float32)
     w2 = (rng.integers(-1, 2, size=(256, 256)) * (rng.random((256, 256)) < 0.02)).astype(np.float32)

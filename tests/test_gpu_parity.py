@@ -194,7 +194,9 @@ def test_d1_policy_sweep_parity(engine):
 
 
 @pytest.mark.parametrize("variant", ["slots16", "delay0", "tol0", "big_load", "neg_load",
-                                     "no_limit_cpu", "behavior", "budget50", "one_pool"])
+                                     "no_limit_cpu", "behavior", "budget50", "one_pool",
+                                     "pdb100", "pdb0", "long_ca", "up_stab", "rules_reordered",
+                                     "min0", "t1", "heavy_delay0"])
 def test_d1_edge_cases(engine, variant):
     spec = configs.config2_world(n_steps=480)
     n = 700
@@ -225,6 +227,31 @@ def test_d1_edge_cases(engine, variant):
         load = load * 5
     elif variant == "one_pool":
         spec.pools = spec.pools[1:]
+    elif variant == "pdb100":  # no voluntary eviction ever allowed: empty nodes only
+        spec.pdb_pct = 100
+        load = load * 4
+    elif variant == "pdb0":
+        spec.pdb_pct = 0
+        load = load * 4
+    elif variant == "long_ca":  # consolidateAfter beyond the 16-bit per-slot field (clamped)
+        for p in spec.pools:
+            p.profile[abi.PROFILE_OFFPEAK].consolidate_after_s = 5_000_000
+        sc.reset_ca_s = np.full(n, 30000, np.int16)
+    elif variant in ("up_stab", "rules_reordered"):  # the generic-behaviour instantiation
+        from ccka.world import default_down, hpa_rules
+        pol = [(abi.HPA_PERCENT, 100, 15), (abi.HPA_PODS, 4, 15)]
+        up = hpa_rules(abi.SELECT_MAX, pol, 120) if variant == "up_stab" else \
+            hpa_rules(abi.SELECT_MAX, pol[::-1], 0)
+        spec.deploys = [deployment(abi.SCALER_HPA, up=up, down=default_down(300))]
+    elif variant == "min0":
+        spec.deploys = [deployment(abi.SCALER_HPA, min_r=0, replicas0=0)]
+        load[(np.arange(spec.n_steps) // 37) % 3 == 0] = 0
+    elif variant == "t1":
+        spec.n_steps = 1
+        load = np.ascontiguousarray(load[:1])
+    elif variant == "heavy_delay0":  # saturated nodes and zero-delay launches together
+        spec.provision_delay_steps = 0
+        load = load * 7
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
     assert engine.last_engine()[0] == 2, variant
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
