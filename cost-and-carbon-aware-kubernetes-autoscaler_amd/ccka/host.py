@@ -35,6 +35,10 @@ def lib():
                                                 C.POINTER(abi.World)]),
             "ccka_host_summary": (C.c_int, [vp, C.POINTER(abi.World), C.POINTER(abi.Results),
                                             C.POINTER(abi.TrajRec), C.c_char_p, C.c_int64]),
+            "ccka_host_export": (C.c_int, [vp, C.c_int32, C.POINTER(abi.World), C.POINTER(abi.TrajRec),
+                                           C.c_int64, C.POINTER(abi.Results), C.c_int64, C.c_int64,
+                                           C.c_int64, C.c_int64, C.c_char_p, C.c_int64,
+                                           C.POINTER(C.c_int64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -46,7 +50,11 @@ def lib():
 
 HOST_EXPORTED = ["ccka_host_open", "ccka_host_close", "ccka_host_last_error", "ccka_host_apply",
                  "ccka_host_patch", "ccka_host_get_json", "ccka_host_policy_patch",
-                 "ccka_host_burst_manifest", "ccka_host_build_world", "ccka_host_summary"]
+                 "ccka_host_burst_manifest", "ccka_host_build_world", "ccka_host_summary",
+                 "ccka_host_export"]
+
+EXPORT_PROMETHEUS = 1
+EXPORT_CSV = 2
 
 
 class Host:
@@ -108,3 +116,29 @@ class Host:
         tp = traj.ctypes.data_as(C.POINTER(abi.TrajRec)) if traj is not None else None
         return self._str(self.L.ccka_host_summary(self.h, C.byref(world), C.byref(results), tp,
                                                   self._buf, len(self._buf)), "summary")
+
+    def export(self, world, results: dict, traj, fmt=EXPORT_PROMETHEUS, s0=0, n=None, first_id=0,
+               start_unix_ms=0) -> str:
+        """Trajectory export (ccka_host_export): Prometheus text exposition or CSV for
+        scenarios [s0, s0 + n) of `traj` ([n_steps][traj_n] TRAJ_DTYPE) and the per-scenario
+        `results` arrays (any subset of abi.RESULT_FIELDS; missing families are omitted)."""
+        import numpy as np
+        traj = np.ascontiguousarray(traj)
+        traj_n = traj.shape[1]
+        n = traj_n - s0 if n is None else n
+        r = abi.Results()
+        keep = []
+        for name, ct, dt in abi.RESULT_FIELDS:
+            if name in results:
+                a = np.ascontiguousarray(results[name], dt)
+                keep.append(a)
+                setattr(r, name, a.ctypes.data_as(C.POINTER(ct)))
+        tp = traj.ctypes.data_as(C.POINTER(abi.TrajRec))
+        need = C.c_int64(0)
+        args = (self.h, fmt, C.byref(world), tp, traj_n, C.byref(r), s0, n, first_id, start_unix_ms)
+        if self.L.ccka_host_export(*args, None, 0, C.byref(need)) != 0 and need.value <= 0:
+            self._err("export")
+        buf = C.create_string_buffer(need.value)
+        if self.L.ccka_host_export(*args, buf, need.value, C.byref(need)) != 0:
+            self._err("export")
+        return buf.raw[:need.value - 1].decode()

@@ -6,10 +6,12 @@
 //       the demo_30 Deployments / demo_10 PDB / our base NodePools (YAML)
 //   ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]...
 //               [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]
-//               [--device D] [--json OUT]
+//               [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]
 //       ingest the manifests, build the world, roll one cluster forward on the
 //       MI355X through libccka (ccka.h) and print the demo_41-style summary
-//       (the reference's missing demo_41_observe_cost_nodes.sh, README.md:57).
+//       (the reference's missing demo_41_observe_cost_nodes.sh, README.md:57);
+//       --prom / --csv write the trajectory as Prometheus text exposition / CSV
+//       (ccka_host_export, the series the reference's observe path scrapes).
 // Environment: NP_SPOT NP_OD OFFPEAK_ZONES PEAK_ZONES NAMESPACE COUNT REPLICAS.
 #include <cstdio>
 #include <cstdlib>
@@ -40,7 +42,7 @@ static int usage() {
                "       ccka manifest <burst [--index I] | pdb | nodepools>\n"
                "       ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]...\n"
                "                   [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]\n"
-               "                   [--device D] [--json OUT]\n");
+               "                   [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]\n");
   return 2;
 }
 
@@ -107,7 +109,8 @@ int main(int argc, char** argv) {
   }
   if (cmd != "replay") return usage();
 
-  std::string nodepools, catalog = "tiny", json_out;
+  std::string nodepools, catalog = "tiny", json_out, prom_out, csv_out;
+  long long start_ms = 0;
   std::vector<std::string> applies;
   std::vector<std::vector<std::string>> patches;
   int steps = 1440, max_nodes = 16, device = 0;
@@ -129,6 +132,9 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[a], "--load-m")) load_m = std::atol(next().c_str());
     else if (!std::strcmp(argv[a], "--device")) device = std::atoi(next().c_str());
     else if (!std::strcmp(argv[a], "--json")) json_out = next();
+    else if (!std::strcmp(argv[a], "--prom")) prom_out = next();
+    else if (!std::strcmp(argv[a], "--csv")) csv_out = next();
+    else if (!std::strcmp(argv[a], "--start-unix-ms")) start_ms = std::atoll(next().c_str());
     else return usage();
   }
   // manifests in: base NodePools, then every applied file; default demand is
@@ -197,6 +203,19 @@ int main(int argc, char** argv) {
                  "\"deletions\": %d, \"peak_nodes\": %d, \"final_replicas\": %d, \"final_nodes\": %d, "
                  "\"last_choice\": %u, \"choice_hash\": %u}\n",
                  (long long)cost, energy, gco2, slo, (long long)pend, nsp, nod, lau, del, peak, frep, fnod, lc, hash);
+    std::fclose(f);
+  }
+  for (int fmt : {CCKA_EXPORT_PROMETHEUS, CCKA_EXPORT_CSV}) {
+    const std::string& path = fmt == CCKA_EXPORT_PROMETHEUS ? prom_out : csv_out;
+    if (path.empty()) continue;
+    int64_t need = 0;
+    ccka_host_export(h, fmt, &w, traj.data(), 1, &r, 0, 1, 0, start_ms, nullptr, 0, &need);
+    std::vector<char> text((size_t)(need > 0 ? need : 1));
+    if (ccka_host_export(h, fmt, &w, traj.data(), 1, &r, 0, 1, 0, start_ms, text.data(), need, &need) != CCKA_OK)
+      die_host(h, "export");
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) return 1;
+    std::fputs(text.data(), f);
     std::fclose(f);
   }
   ccka_close(ctx);

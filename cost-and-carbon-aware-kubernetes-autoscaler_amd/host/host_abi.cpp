@@ -161,4 +161,148 @@ int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
   });
 }
 
+int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const ccka_traj_rec* traj,
+                     int64_t traj_n, const ccka_results* r, int64_t s0, int64_t n, int64_t first_id,
+                     int64_t start_unix_ms, char* out, int64_t cap, int64_t* needed) {
+  return guarded(h, [&] {
+    if (needed) *needed = 0;
+    if (!w || !traj || !r || n < 0 || s0 < 0 || s0 + n > traj_n || w->n_steps < 1 ||
+        (format != CCKA_EXPORT_PROMETHEUS && format != CCKA_EXPORT_CSV))
+      return (int)CCKA_EINVAL;
+    const int T = w->n_steps;
+    const int start = ((w->start_minute % 1440) + 1440) % 1440;
+    auto rec = [&](int t, int64_t s) -> const ccka_traj_rec& { return traj[(int64_t)t * traj_n + s0 + s]; };
+    std::string o;
+    char b[512];
+    if (format == CCKA_EXPORT_CSV) {
+      o.reserve((size_t)(n * T * 40 + 128));
+      o += "scenario,step,minute,replicas,pending,nodes_spot,nodes_od,last_type,flags\n";
+      for (int64_t s = 0; s < n; ++s)
+        for (int t = 0; t < T; ++t) {
+          const ccka_traj_rec& x = rec(t, s);
+          std::snprintf(b, sizeof b, "%lld,%d,%d,%d,%d,%u,%u,%u,%u\n", (long long)(first_id + s0 + s), t,
+                        (start + t) % 1440, x.replicas, x.pending, x.nodes_spot, x.nodes_od, x.last_type, x.flags);
+          o += b;
+        }
+    } else {
+      o.reserve((size_t)(n * T * 7 * 110 + 4096));
+      const std::string ns = h->env.ns;
+      const std::string dep = w->n_deploy == 1 && !h->meta.deploy_names.empty() ? h->meta.deploy_names[0]
+                              : w->n_deploy == 1                                 ? std::string("deployment-0")
+                                                                                 : std::string("all");
+      auto family = [&](const char* name, const char* type, const char* help) {
+        std::snprintf(b, sizeof b, "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
+        o += b;
+      };
+      auto ts = [&](int t) { return (long long)(start_unix_ms + (int64_t)t * CCKA_STEP_SECONDS * 1000); };
+      auto dep_series = [&](const char* name, const char* type, const char* help, auto value) {
+        family(name, type, help);
+        for (int64_t s = 0; s < n; ++s)
+          for (int t = 0; t < T; ++t) {
+            std::snprintf(b, sizeof b, "%s{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %lld %lld\n", name,
+                          ns.c_str(), dep.c_str(), (long long)(first_id + s0 + s), (long long)value(rec(t, s)), ts(t));
+            o += b;
+          }
+      };
+      dep_series("kube_deployment_spec_replicas", "gauge", "Number of desired pods for a deployment.",
+                 [](const ccka_traj_rec& x) { return (long long)x.replicas; });
+      dep_series("kube_deployment_status_replicas_available", "gauge",
+                 "The number of available (running) replicas per deployment.",
+                 [](const ccka_traj_rec& x) { return (long long)x.replicas - x.pending; });
+      dep_series("kube_deployment_status_replicas_unavailable", "gauge",
+                 "The number of unavailable (pending) replicas per deployment.",
+                 [](const ccka_traj_rec& x) { return (long long)x.pending; });
+      family("ccka_nodes", "gauge", "Karpenter nodes of the scenario by capacity type.");
+      for (int c = 0; c < 2; ++c)
+        for (int64_t s = 0; s < n; ++s)
+          for (int t = 0; t < T; ++t) {
+            const ccka_traj_rec& x = rec(t, s);
+            std::snprintf(b, sizeof b, "ccka_nodes{scenario=\"%lld\",capacity_type=\"%s\"} %u %lld\n",
+                          (long long)(first_id + s0 + s), c == 0 ? "spot" : "on-demand",
+                          c == 0 ? (unsigned)x.nodes_spot : (unsigned)x.nodes_od, ts(t));
+            o += b;
+          }
+      family("ccka_policy_profile", "gauge", "1 while the peak NodePool profile is applied, 0 off-peak.");
+      for (int64_t s = 0; s < n; ++s)
+        for (int t = 0; t < T; ++t) {
+          std::snprintf(b, sizeof b, "ccka_policy_profile{scenario=\"%lld\"} %u %lld\n", (long long)(first_id + s0 + s),
+                        rec(t, s).flags & 1u, ts(t));
+          o += b;
+        }
+      family("ccka_step_event", "gauge", "1 when the step launched a node, deleted a node or violated the SLO.");
+      static const char* ev[3] = {"launch", "deletion", "slo_violation"};
+      for (int e = 0; e < 3; ++e)
+        for (int64_t s = 0; s < n; ++s)
+          for (int t = 0; t < T; ++t) {
+            std::snprintf(b, sizeof b, "ccka_step_event{scenario=\"%lld\",event=\"%s\"} %u %lld\n",
+                          (long long)(first_id + s0 + s), ev[e], (rec(t, s).flags >> (e + 1)) & 1u, ts(t));
+            o += b;
+          }
+      // run totals at the last step
+      auto total = [&](const char* name, const char* type, const char* help, const char* extra, auto value) {
+        family(name, type, help);
+        for (int64_t s = 0; s < n; ++s) {
+          std::snprintf(b, sizeof b, "%s{scenario=\"%lld\"%s} %.17g %lld\n", name, (long long)(first_id + s0 + s), extra,
+                        (double)value(s0 + s), ts(T - 1));
+          o += b;
+        }
+      };
+      if (r->cost_uphmin)
+        total("ccka_cost_dollars_total", "counter", "Node cost of the run (cloud prices, per-minute billing).", "",
+              [&](int64_t i) { return (double)r->cost_uphmin[i] / 6e7; });
+      if (r->energy_wmin)
+        total("ccka_energy_kwh_total", "counter", "Node energy of the run.", "",
+              [&](int64_t i) { return r->energy_wmin[i] / 6e4; });
+      if (r->gco2)
+        total("ccka_carbon_grams_total", "counter", "Operational carbon of the run (hourly grid intensity).", "",
+              [&](int64_t i) { return r->gco2[i]; });
+      if (r->slo_minutes)
+        total("ccka_slo_violation_minutes_total", "counter", "Minutes with pending pods or utilisation above the SLO.",
+              "", [&](int64_t i) { return (double)r->slo_minutes[i]; });
+      if (r->pending_pod_minutes)
+        total("ccka_pending_pod_minutes_total", "counter", "Pending pod-minutes of the run.", "",
+              [&](int64_t i) { return (double)r->pending_pod_minutes[i]; });
+      if (r->node_min_spot && r->node_min_od) {
+        family("ccka_node_minutes_total", "counter", "Karpenter node-minutes of the run by capacity type.");
+        for (int c = 0; c < 2; ++c)
+          for (int64_t s = 0; s < n; ++s) {
+            std::snprintf(b, sizeof b, "ccka_node_minutes_total{scenario=\"%lld\",capacity_type=\"%s\"} %d %lld\n",
+                          (long long)(first_id + s0 + s), c == 0 ? "spot" : "on-demand",
+                          c == 0 ? r->node_min_spot[s0 + s] : r->node_min_od[s0 + s], ts(T - 1));
+            o += b;
+          }
+      }
+      if (r->launches)
+        total("ccka_launches_total", "counter", "NodeClaims launched.", "",
+              [&](int64_t i) { return (double)r->launches[i]; });
+      if (r->deletions)
+        total("ccka_deletions_total", "counter", "Nodes removed by consolidation.", "",
+              [&](int64_t i) { return (double)r->deletions[i]; });
+      if (r->cost_uphmin) {
+        // OpenCost-style allocation: the run's node cost over its running pod-hours
+        family("ccka_pod_cost_dollars_per_hour", "gauge",
+               "Node cost allocated per running pod-hour (cost / available pod-hours).");
+        for (int64_t s = 0; s < n; ++s) {
+          long long pod_min = 0;
+          for (int t = 0; t < T; ++t) pod_min += (long long)rec(t, s).replicas - rec(t, s).pending;
+          if (pod_min <= 0) continue;
+          std::snprintf(b, sizeof b,
+                        "ccka_pod_cost_dollars_per_hour{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %.17g %lld\n",
+                        ns.c_str(), dep.c_str(), (long long)(first_id + s0 + s),
+                        ((double)r->cost_uphmin[s0 + s] / 6e7) / ((double)pod_min / 60.0), ts(T - 1));
+          o += b;
+        }
+      }
+    }
+    if (needed) *needed = (int64_t)o.size() + 1;
+    if (!out || (int64_t)o.size() + 1 > cap) {
+      h->err = "output buffer too small: need " + std::to_string(o.size() + 1);
+      return (int)CCKA_EINVAL;
+    }
+    std::memcpy(out, o.data(), o.size());
+    out[o.size()] = 0;
+    return (int)CCKA_OK;
+  });
+}
+
 }  // extern "C"

@@ -61,6 +61,27 @@ int ccka_host_build_world(ccka_host* h, const char* catalog, int32_t n_steps, in
 int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
                       const ccka_traj_rec* traj, char* out, int64_t cap);
 
+/* Trajectory export, the downstream wire format of the reference's observe
+ * path (kube-state-metrics scraped into Prometheus/AMP for Grafana and
+ * OpenCost: 06_opencost.sh:318-341,404-432, demo_40_watch_config.sh:51-72).
+ * Scenarios [s0, s0 + n) of a trajectory laid out [n_steps][traj_n] and of
+ * results arrays indexed by scenario (global id = first_id + scenario).
+ *   CCKA_EXPORT_PROMETHEUS: text exposition format, one sample per step at
+ *     start_unix_ms + 60000 t: kube_deployment_spec_replicas,
+ *     kube_deployment_status_replicas_available / _unavailable, ccka_nodes
+ *     {capacity_type}, ccka_policy_profile, ccka_step_event{event}; run
+ *     totals at the last step (cost, energy, carbon, SLO minutes, pending
+ *     pod-minutes, node-minutes, launches, deletions) and the OpenCost-style
+ *     allocation ccka_pod_cost_dollars_per_hour = cost / available pod-hours.
+ *   CCKA_EXPORT_CSV: scenario,step,minute,replicas,pending,nodes_spot,
+ *     nodes_od,last_type,flags.
+ * *needed = bytes required including the terminating NUL; CCKA_EINVAL (with
+ * *needed set) when out is NULL or cap is smaller. */
+enum { CCKA_EXPORT_PROMETHEUS = 1, CCKA_EXPORT_CSV = 2 };
+int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const ccka_traj_rec* traj,
+                     int64_t traj_n, const ccka_results* r, int64_t s0, int64_t n, int64_t first_id,
+                     int64_t start_unix_ms, char* out, int64_t cap, int64_t* needed);
+
 #ifdef __cplusplus
 }
 #endif

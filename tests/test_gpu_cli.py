@@ -20,7 +20,9 @@ pytestmark = pytest.mark.gpu
 def test_cli_replay_matches_oracle(tmp_path, load_m, catalog):
     out = tmp_path / "r.json"
     env = {k: v for k, v in os.environ.items() if k not in ("COUNT", "REPLICAS", "NP_SPOT", "NP_OD")}
-    txt = subprocess.run([CLI, "replay", "--catalog", catalog, "--load-m", str(load_m), "--json", str(out)],
+    prom = tmp_path / "r.prom"
+    txt = subprocess.run([CLI, "replay", "--catalog", catalog, "--load-m", str(load_m), "--json", str(out),
+                          "--prom", str(prom)],
                          env=env, check=True, capture_output=True, text=True, timeout=120).stdout
     assert "cost=$" in txt and "spot-preferred" in txt
     got = json.load(open(out))
@@ -36,3 +38,6 @@ def test_cli_replay_matches_oracle(tmp_path, load_m, catalog):
         assert got[f] == int(want[f][0]), f
     for f in ("energy_wmin", "gco2"):
         assert got[f] == float(want[f][0]), f
+    # the exported run totals are the same results
+    lines = [ln for ln in open(prom).read().splitlines() if ln.startswith("ccka_launches_total{")]
+    assert len(lines) == 1 and float(lines[0].split()[1]) == got["launches"]
