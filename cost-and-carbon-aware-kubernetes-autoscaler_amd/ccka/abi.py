@@ -77,7 +77,7 @@ class World(C.Structure):
                 ("base_util", C.c_double), ("carbon_weight", C.c_double),
                 ("pdb_min_available_pct", C.c_int32), ("peak_start_min", C.c_int32),
                 ("peak_end_min", C.c_int32), ("peak_switch", C.c_int32),
-                ("reset_ca_s", C.c_int32), ("_pad", C.c_int32)]
+                ("reset_ca_s", C.c_int32), ("drift", C.c_int32)]
 
 
 class Scenarios(C.Structure):

@@ -286,6 +286,7 @@ class WorldSpec:
     peak_switch: int = 1
     reset_ca_s: int = 30
     carbon_weight: float = 0.0
+    drift: int = 0
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -331,6 +332,7 @@ class WorldSpec:
         w.peak_end_min = self.peak_end
         w.peak_switch = self.peak_switch
         w.reset_ca_s = self.reset_ca_s
+        w.drift = self.drift
         return w
 
 

@@ -396,6 +396,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     plimit[q] = gw->pools[q].limit_cpu_m;
   }
   const int pdb_pct = gw->pdb_min_available_pct;
+  const bool gdrift = gw->drift != 0;
   const int slo_util = gw->slo_util_pct;
   const int base_nodes = gw->base_nodes, base_type = gw->base_type;
 
@@ -884,6 +885,20 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           }
           allowed = max(rdyp - ((long long)pdb_pct * reps + 99) / 100, 0LL);
         }
+        // drifted nodes (SEMANTICS 3.G0): zone / capacity type outside the
+        // pool's current requirements
+        uint32_t dmask = 0;
+        if (gdrift) {
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            const uint32_t x = ninfo[n];
+            uint32_t zm = 0, cm = 0;
+#pragma unroll
+            for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+              if (qq == ni_pool(x)) { zm = pzm[qq]; cm = pcm[qq]; }
+            if ((used >> n & 1u) && (!(zm >> ni_zone(x) & 1u) || !(cm & capbit(ni_cap(x))))) dmask |= 1u << n;
+          }
+        }
         for (int q = 0; q < NP; ++q) {
           int npool = 0, qbudget = 0, qca = 0, qpol = 0;
 #pragma unroll
@@ -894,6 +909,82 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           if (npool == 0) continue;
           const int budget = (qbudget * npool + 99) / 100;
           int deleted = 0;
+          // ---- G0. drift: slot order, shares the pool budget, no consolidateAfter ----
+          if (dmask) {
+            uint32_t pq = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) pq |= (ni_pool(ninfo[n]) == q ? 1u : 0u) << n;
+            uint32_t cand = dmask & rdy & pq;
+            while (cand && deleted < budget) {
+              const int best = __builtin_ctz(cand);
+              cand &= cand - 1u;
+              int bp[DMAX];
+              long long pdb_pods = 0;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                bp[d] = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) if (n == best) bp[d] = npods[n][d];
+                if (d < D && dep[d].pdb) pdb_pods += bp[d];
+              }
+              if (pdb_pods > allowed) continue;
+              // pods move first-fit onto ready, non-drifted nodes; the rest are
+              // evicted (Pending until E/F of a later step)
+              const uint32_t recv = rdy & ~dmask;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                if (d >= D) break;
+                int need_d = bp[d];
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) {
+                  const uint32_t x = ninfo[n];
+                  if (need_d > 0 && (recv >> n & 1u) && (capbit(ni_cap(x)) & capsel[d])) {
+                    int f;
+                    if (DMAX == 1) {
+                      f = ncap[n] - npods[n][0];
+                    } else {
+                      int sc = 0, sm = 0, sp = 0;
+#pragma unroll
+                      for (int e = 0; e < DMAX; ++e) {
+                        if (e >= D) break;
+                        sc += npods[n][e] * dep[e].req_cpu;
+                        sm += npods[n][e] * dep[e].req_mem;
+                        sp += npods[n][e];
+                      }
+                      f = max(type_fit<DMAX>(L, ni_type(x), sc, sm, sp, dep[d].req_cpu, dep[d].req_mem), 0);
+                    }
+                    const int k = min(f, need_d);
+                    if (k > 0) { npods[n][d] += k; need_d -= k; nlast[n] = t; }
+                  }
+                }
+                rpods[d] -= need_d;
+                placed[d] -= need_d;
+              }
+              int bprice = 0;
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                if (n == best) {
+                  bprice = nprice[n];
+                  if (ni_cap(ninfo[n]) == 0) nsp--; else nod--;
+#pragma unroll
+                  for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+                    if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
+                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+#pragma unroll
+                  for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
+                }
+              }
+              burn -= bprice;
+              used &= ~(1u << best);
+              rdy &= ~(1u << best);
+              dmask &= ~(1u << best);
+              allowed -= pdb_pods;
+              deleted++;
+              deletions++;
+              any_deleted = true;
+              flags |= 4u | 16u;
+            }
+          }
           if (DMAX == 1) {
             // identical pods: a candidate's pods fit first-fit on the other
             // compatible ready nodes iff their free capacities add up, so one
@@ -1077,7 +1168,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             flags |= 4u;
           }
         }
-        g_dirty = budget_hit || any_deleted;
+        g_dirty = budget_hit || any_deleted || dmask != 0;
         // next step at which a node becomes a new candidate (consolidatable and ready)
         int wake = 0x7fffffff;
 #pragma unroll

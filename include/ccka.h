@@ -159,7 +159,9 @@ typedef struct ccka_world {
   int32_t peak_end_min;
   int32_t peak_switch;          /* 1: peak/off-peak switch on            */
   int32_t reset_ca_s;           /* consolidateAfter of the RESET profile */
-  int32_t _pad;
+  int32_t drift;                /* 1: Karpenter drift disruption on a zone /
+                                   capacity-type requirement change
+                                   (docs/SEMANTICS.md 3.G0) */
 } ccka_world;
 
 /* Per-scenario parameters, SoA, host pointers. NULL ⇒ world default. */

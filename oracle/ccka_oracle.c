@@ -324,6 +324,13 @@ typedef struct {
   uint32_t last_choice, hash;
 } o_state;
 
+/* Karpenter drift: the node's zone or capacity type no longer satisfies its
+ * pool's (patched) requirements. */
+static int o_drifted(const o_state* st, const o_node* nd) {
+  const o_pool* pl = &st->pools[nd->pool];
+  return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
+}
+
 static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* load, int64_t i,
                       int64_t nsc, ccka_results* out, ccka_traj_rec* traj) {
   const ccka_world* w = e->w;
@@ -634,6 +641,35 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
         if (npool == 0) continue;
         const int budget = (w->pools[p].budget_pct * npool + 99) / 100;
         int deleted = 0;
+        /* G0. drift (docs/SEMANTICS.md 3.G0): ready nodes whose zone or
+         * capacity type left the pool's requirements after the patch of
+         * demo_20_offpeak_configure.sh:64-81 / demo_21_peak_configure.sh:60-77,
+         * slot order, sharing this pool's budget; no consolidateAfter wait */
+        for (int n = 0; w->drift && n < NN && deleted < budget; ++n) {
+          o_node* dn = &st.nodes[n];
+          if (!dn->used || dn->pool != p || dn->ready_step > t || !o_drifted(&st, dn)) continue;
+          int64_t pdb_pods = 0;
+          for (int d = 0; d < D; ++d) if (w->deploy[d].pdb_member) pdb_pods += dn->pods[d];
+          if (pdb_pods > allowed) continue;
+          /* pods move first-fit onto ready, non-drifted nodes; the rest are
+           * evicted and Pending until F places or provisions them */
+          for (int d = 0; d < D; ++d) {
+            int need = dn->pods[d];
+            for (int m = 0; m < NN && need > 0; ++m) {
+              o_node* nd = &st.nodes[m];
+              if (m == n || !nd->used || nd->ready_step > t || o_drifted(&st, nd)) continue;
+              if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
+              const int64_t f = o_node_fit(e, nd, d);
+              const int k = (int)(f < need ? f : need);
+              if (k > 0) { nd->pods[d] += k; need -= k; nd->last_event = t; }
+            }
+          }
+          memset(dn, 0, sizeof(o_node));
+          allowed -= pdb_pods;
+          deleted++;
+          st.deletions++;
+          flags |= 4 | 16;
+        }
         int rejected[CCKA_MAX_NODES] = {0};
         while (deleted < budget) {
           int best = -1, bpods = 0;

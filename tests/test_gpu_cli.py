@@ -16,13 +16,13 @@ from parity import INT_FIELDS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("load_m,catalog", [(100, "tiny"), (450, "small")])
-def test_cli_replay_matches_oracle(tmp_path, load_m, catalog):
+@pytest.mark.parametrize("load_m,catalog,drift", [(100, "tiny", 0), (450, "small", 0), (450, "small", 1)])
+def test_cli_replay_matches_oracle(tmp_path, load_m, catalog, drift):
     out = tmp_path / "r.json"
     env = {k: v for k, v in os.environ.items() if k not in ("COUNT", "REPLICAS", "NP_SPOT", "NP_OD")}
     prom = tmp_path / "r.prom"
     txt = subprocess.run([CLI, "replay", "--catalog", catalog, "--load-m", str(load_m), "--json", str(out),
-                          "--prom", str(prom)],
+                          "--prom", str(prom)] + (["--drift"] if drift else []),
                          env=env, check=True, capture_output=True, text=True, timeout=120).stdout
     assert "cost=$" in txt and "spot-preferred" in txt
     got = json.load(open(out))
@@ -32,6 +32,7 @@ def test_cli_replay_matches_oracle(tmp_path, load_m, catalog):
         h.apply(h.manifest(i))
     h.apply(h.manifest(0))
     w = h.build_world(catalog, 1440, 16)
+    w.drift = drift
     load = np.full((1440, 12, 1), load_m, np.int32)
     want, _ = po.rollout_world(w, ScenarioSet(1), load)
     for f in INT_FIELDS:

@@ -273,3 +273,47 @@ def test_d1_matches_general_kernel(engine):
     finally:
         engine.set_engine(0)
     compare(r2, r1, t2, t1)
+
+
+# ---------------------------------------------------------------------------
+# Karpenter drift on the peak/off-peak zone switch (SEMANTICS 3.G0)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("variant", ["pdb50", "no_pdb", "budget50", "wrap_peak"])
+def test_drift_parity_single_deployment(engine, variant):
+    spec = configs.config2_world(n_steps=1440)
+    spec.drift = 1
+    n = 1537
+    sc = configs.hpa_scenarios(n, first_id=901)
+    if variant == "no_pdb":
+        spec.pdb_pct = -1
+    elif variant == "budget50":
+        for p in spec.pools:
+            p.budget_pct = 50
+    elif variant == "wrap_peak":
+        spec.peak_start, spec.peak_end, spec.start_minute = 1300, 200, 1200
+        spec.pdb_pct = -1
+    load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=sc.first_id)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 1  # drift runs on the general kernel
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert ((tc["flags"] & 16) != 0).any()  # drift deletions happened
+    compare(rg, rc, tg, tc)
+
+
+def test_drift_parity_multi_deployment(engine):
+    spec = configs.config2_world(max_nodes=12)
+    spec.drift = 1
+    spec.pdb_pct = -1
+    spec.deploys = [
+        deployment(abi.SCALER_HPA, cap_sel=abi.CAP_SPOT),
+        deployment(abi.SCALER_HPA, req_cpu=500, req_mem=512, limit_cpu=1000, cap_sel=abi.CAP_OD, target=60),
+        deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=800, keda_activation=1500,
+                   keda_cooldown=300, cap_sel=abi.CAP_SPOT | abi.CAP_OD),
+    ]
+    n = 700
+    sc = ScenarioSet(n)
+    load = po.gen_load(configs.trace_gen(9), spec.n_steps, 3, n)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert ((tc["flags"] & 16) != 0).any()
+    compare(rg, rc, tg, tc)

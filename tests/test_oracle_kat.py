@@ -291,3 +291,39 @@ def test_pareto_known_answer():
           "slo_minutes": np.array([0, 0, 0, 1, 9])}
     # 2 is dominated by 1 (equal carbon/SLO, cheaper); 3 by 1; 1 == itself kept
     assert po.pareto(st).tolist() == [0, 1, 4]
+
+
+# ---------------------------------------------------------------- drift (SEMANTICS §3.G0)
+def test_drift_evicts_and_reprovisions_in_peak_zone():
+    """5 static spot pods launch in us-east-2a (off-peak) at t=0. At t=10 the
+    clock reaches 16:00 and PEAK narrows the zones to us-east-2c: with drift on
+    the node is deleted (no consolidateAfter wait), its pods are Pending at
+    t=10, re-provisioned at t=11 in zone c and running at t=12. Without drift
+    the node stays in zone a."""
+    d = deployment(abi.SCALER_STATIC, replicas0=5, min_r=5, max_r=5)
+    spec = tiny_world([d], T=40, start_minute=950, pdb_pct=-1, drift=1)
+    load = np.zeros((40, 1, 1), np.int32)
+    r, tr = run(spec, load)
+    assert r["launches"][0] == 2 and r["deletions"][0] == 1
+    assert (r["last_choice"][0] >> 12) & 3 == 2              # us-east-2c
+    flags = tr["flags"][:, 0]
+    assert (flags[10] & 16) and (flags[10] & 4) and not (flags[:10] & 16).any()
+    assert list(tr["pending"][9:13, 0]) == [0, 5, 5, 0]
+    spec.drift = 0
+    r0, tr0 = run(spec, load)
+    assert r0["launches"][0] == 1 and r0["deletions"][0] == 0
+    assert (r0["last_choice"][0] >> 12) & 3 == 0 and (tr0["pending"][1:, 0] == 0).all()
+
+
+def test_drift_blocked_by_pdb_and_budget():
+    """minAvailable 50 % of 5 ready pods allows 2 evictions < 5 on the node:
+    the drifted node is kept. A 0 % budget also blocks drift."""
+    d = deployment(abi.SCALER_STATIC, replicas0=5, min_r=5, max_r=5)
+    spec = tiny_world([d], T=30, start_minute=950, pdb_pct=50, drift=1)
+    r, tr = run(spec, np.zeros((30, 1, 1), np.int32))
+    assert r["deletions"][0] == 0 and (tr["pending"][1:, 0] == 0).all()
+    spec = tiny_world([d], T=30, start_minute=950, pdb_pct=-1, drift=1)
+    for p in spec.pools:
+        p.budget_pct = 0
+    r, _ = run(spec, np.zeros((30, 1, 1), np.int32))
+    assert r["deletions"][0] == 0 and r["launches"][0] == 1
