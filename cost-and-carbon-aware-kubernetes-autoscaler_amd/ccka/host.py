@@ -39,6 +39,8 @@ def lib():
                                            C.c_int64, C.POINTER(abi.Results), C.c_int64, C.c_int64,
                                            C.c_int64, C.c_int64, C.c_char_p, C.c_int64,
                                            C.POINTER(C.c_int64)]),
+            "ccka_host_set_admission": (C.c_int, [vp, C.c_uint32]),
+            "ccka_host_admission_review": (C.c_int, [vp, C.c_uint32, C.c_char_p, C.c_char_p, C.c_int64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -51,7 +53,12 @@ def lib():
 HOST_EXPORTED = ["ccka_host_open", "ccka_host_close", "ccka_host_last_error", "ccka_host_apply",
                  "ccka_host_patch", "ccka_host_get_json", "ccka_host_policy_patch",
                  "ccka_host_burst_manifest", "ccka_host_build_world", "ccka_host_summary",
-                 "ccka_host_export"]
+                 "ccka_host_export", "ccka_host_set_admission", "ccka_host_admission_review"]
+
+# Kyverno guard policies (04_kyverno.sh:24-75), ccka_host.h CCKA_ADMIT_*
+ADMIT_REQUIRE_REQUESTS_LIMITS = 1
+ADMIT_CRITICAL_NO_SPOT = 2
+ADMIT_ALL = ADMIT_REQUIRE_REQUESTS_LIMITS | ADMIT_CRITICAL_NO_SPOT
 
 EXPORT_PROMETHEUS = 1
 EXPORT_CSV = 2
@@ -88,6 +95,17 @@ class Host:
     def apply(self, yaml_text: str):
         if self.L.ccka_host_apply(self.h, yaml_text.encode()) != 0:
             self._err("apply")
+
+    def set_admission(self, policies: int):
+        if self.L.ccka_host_set_admission(self.h, policies) != 0:
+            self._err("set_admission")
+
+    def admission_review(self, yaml_text: str, policies: int = ADMIT_ALL) -> list:
+        """Dry run: the violations of every document, [{kind, name, policy, rule, message, path}]."""
+        import json
+        return json.loads(self._str(self.L.ccka_host_admission_review(self.h, policies, yaml_text.encode(),
+                                                                      self._buf, len(self._buf)),
+                                    "admission_review"))
 
     def patch(self, kind, name, ptype, text):
         if self.L.ccka_host_patch(self.h, kind.encode(), name.encode(), ptype.encode(), text.encode()) != 0:

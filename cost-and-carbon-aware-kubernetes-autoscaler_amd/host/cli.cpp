@@ -43,7 +43,7 @@ static int usage() {
                "       ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]...\n"
                "                   [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]\n"
                "                   [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]\n"
-               "                   [--drift]\n");
+               "                   [--drift] [--kyverno]\n");
   return 2;
 }
 
@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
   long long start_ms = 0;
   std::vector<std::string> applies;
   std::vector<std::vector<std::string>> patches;
-  int steps = 1440, max_nodes = 16, device = 0, drift = 0;
+  int steps = 1440, max_nodes = 16, device = 0, drift = 0, kyverno = 0;
   long load_m = 100;
   for (int a = 2; a < argc; ++a) {
     auto next = [&]() -> std::string {
@@ -137,10 +137,14 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[a], "--csv")) csv_out = next();
     else if (!std::strcmp(argv[a], "--start-unix-ms")) start_ms = std::atoll(next().c_str());
     else if (!std::strcmp(argv[a], "--drift")) drift = 1;
+    else if (!std::strcmp(argv[a], "--kyverno")) kyverno = 1;
     else return usage();
   }
   // manifests in: base NodePools, then every applied file; default demand is
   // the demo_30 burst + the demo_10 PDB when no Deployment was applied
+  // 04_kyverno.sh guard policies as the admission pre-filter (opt-in)
+  if (kyverno && ccka_host_set_admission(h, CCKA_ADMIT_REQUIRE_REQUESTS_LIMITS | CCKA_ADMIT_CRITICAL_NO_SPOT) != CCKA_OK)
+    die_host(h, "kyverno");
   if (!nodepools.empty()) {
     if (ccka_host_apply(h, slurp(nodepools).c_str()) != CCKA_OK) die_host(h, nodepools.c_str());
   } else {

@@ -5,6 +5,7 @@
 #include <string>
 
 #include "../../include/ccka_host.h"
+#include "admission.h"
 #include "model.h"
 #include "policy.h"
 
@@ -16,6 +17,7 @@ struct ccka_host {
   Tables tables;
   WorldMeta meta;
   std::string err;
+  uint32_t admission = 0;  // Kyverno policies enforced at apply (CCKA_ADMIT_*)
 };
 
 static int put(ccka_host* h, const std::string& s, char* out, int64_t cap) {
@@ -55,7 +57,40 @@ void ccka_host_close(ccka_host* h) { delete h; }
 const char* ccka_host_last_error(const ccka_host* h) { return h ? h->err.c_str() : "null handle"; }
 
 int ccka_host_apply(ccka_host* h, const char* yaml) {
-  return guarded(h, [&] { h->store.apply(yaml ? yaml : ""); return CCKA_OK; });
+  return guarded(h, [&] { h->store.apply(yaml ? yaml : "", h->admission); return CCKA_OK; });
+}
+
+int ccka_host_set_admission(ccka_host* h, uint32_t policies) {
+  return guarded(h, [&] {
+    if (policies & ~(uint32_t)(CCKA_ADMIT_REQUIRE_REQUESTS_LIMITS | CCKA_ADMIT_CRITICAL_NO_SPOT)) {
+      h->err = "unknown admission policy bits";
+      return (int)CCKA_EINVAL;
+    }
+    h->admission = policies;
+    return (int)CCKA_OK;
+  });
+}
+
+int ccka_host_admission_review(ccka_host* h, uint32_t policies, const char* yaml, char* out, int64_t cap) {
+  return guarded(h, [&] {
+    Value arr = Value::array();
+    for (const Value& doc : parse_yaml_documents(yaml ? yaml : "")) {
+      if (!doc.is_map()) continue;
+      for (const Violation& v : admission_review(doc, policies)) {
+        Value o = Value::object();
+        const Value* k = doc.get("kind");
+        const Value* n = doc.at({"metadata", "name"});
+        o.set("kind", Value::str(k ? k->as_string() : ""));
+        o.set("name", Value::str(n ? n->as_string() : ""));
+        o.set("policy", Value::str(v.policy));
+        o.set("rule", Value::str(v.rule));
+        o.set("message", Value::str(v.message));
+        o.set("path", Value::str(v.path));
+        arr.seq.push_back(o);
+      }
+    }
+    return put(h, to_json(arr), out, cap);
+  });
 }
 
 int ccka_host_patch(ccka_host* h, const char* kind, const char* name, const char* type, const char* patch) {

@@ -1,6 +1,8 @@
 // model.cpp — see model.h.
 #include "model.h"
 
+#include "admission.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -33,14 +35,22 @@ std::vector<const Value*> ManifestStore::all(const std::string& kind) const {
   return out;
 }
 
-void ManifestStore::apply(const std::string& yaml_text) {
+void ManifestStore::apply(const std::string& yaml_text, uint32_t admission) {
+  std::string denied;
   for (auto& doc : parse_yaml_documents(yaml_text)) {
     if (!doc.is_map()) continue;
     const std::string k = kind_of(doc), n = name_of(doc);
     if (k.empty() || n.empty()) throw ParseError("apply: document without kind/metadata.name");
+    const std::vector<Violation> v = admission_review(doc, admission);
+    if (!v.empty()) {
+      denied += (denied.empty() ? "" : "\n") + ("Error from server: error when creating \"" + n + "\": ") +
+                denial_message(doc, v);
+      continue;
+    }
     if (Value* cur = find(k, n)) *cur = doc;
     else objs_.push_back(doc);
   }
+  if (!denied.empty()) throw ParseError(denied);
 }
 
 void ManifestStore::patch(const std::string& kind, const std::string& name, const std::string& type,

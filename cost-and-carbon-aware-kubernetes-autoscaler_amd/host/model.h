@@ -20,8 +20,11 @@ namespace ccka::host {
 
 class ManifestStore {
  public:
-  // kubectl apply -f: upsert every document by (kind, metadata.name)
-  void apply(const std::string& yaml_text);
+  // kubectl apply -f: upsert every document by (kind, metadata.name).
+  // `admission` (kAdmit* bits, admission.h): documents the enabled Kyverno
+  // policies deny are not stored; the others are, and then ParseError carries
+  // the denials (kubectl applies each document independently)
+  void apply(const std::string& yaml_text, uint32_t admission = 0);
   // kubectl patch <kind> <name> --type=merge|json; throws ParseError
   void patch(const std::string& kind, const std::string& name, const std::string& type,
              const std::string& patch_text);

@@ -45,6 +45,18 @@ int ccka_host_patch(ccka_host* h, const char* kind, const char* name, const char
                     const char* patch);
 int ccka_host_get_json(ccka_host* h, const char* kind, const char* name, char* out, int64_t cap);
 
+/* Kyverno guard policies of 04_kyverno.sh:24-75 (enforce mode, auto-gen for
+ * pod controllers) as an admission pre-filter on ccka_host_apply: a denied
+ * document is not stored and apply returns CCKA_EINVAL with kubectl's denial
+ * text in ccka_host_last_error (the admitted documents of the same call are
+ * stored). Off by default: the reference disables the stage (README.md:42). */
+#define CCKA_ADMIT_REQUIRE_REQUESTS_LIMITS 1u /* require-requests-limits      :24-42 */
+#define CCKA_ADMIT_CRITICAL_NO_SPOT 2u        /* critical-no-spot-without-pdb :44-72 */
+int ccka_host_set_admission(ccka_host* h, uint32_t policies);
+/* dry run: JSON array of {kind,name,policy,rule,message,path} violations of
+ * every document in `yaml` under `policies`; length written (excl. NUL) */
+int ccka_host_admission_review(ccka_host* h, uint32_t policies, const char* yaml, char* out, int64_t cap);
+
 /* profile: CCKA_PROFILE_*; json_patch 0 -> the merge patch, 1 -> the
  * requirements JSON Patch (fallback 1: /spec/template path) */
 int ccka_host_policy_patch(ccka_host* h, int32_t profile, const char* pool, int32_t json_patch,
