@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--mode", choices=["trajectory", "summary"], default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--drift", action="store_true",
+                    help="configs 2-4 with Karpenter drift at the zone switch (SEMANTICS 3.G0; general kernel)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,6 +115,7 @@ def main():
             sc = configs.config4_scenarios(rank * grids, grids, ntr)
             gen = configs.config4_trace_gen()
             traj = (args.mode or "summary") == "trajectory"
+        spec.drift = int(args.drift)
         eng.set_world(spec)
         eng.set_scenarios(sc)
         eng.gen_load(gen)
@@ -205,18 +208,20 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True,
             "scaling": "strong" if cfg == 3 else "weak", "vs_baseline": None, "dtype": "int32+int64+f64",
             "data": "synthetic (on-device Philox load traces, seed 20251205)",
-            "config": {"workload": workloads[cfg], "scenarios_per_gpu": N, "steps_per_rollout": T,
+            "config": {"workload": workloads[cfg] + (" + Karpenter drift at the zone switch" if args.drift else ""),
+                       "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
                        "parallelism": f"scenario-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": measured_traffic(cfg, traj, N, T),
+                         "traffic": None if args.drift else measured_traffic(cfg, traj, N, T),
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},
             # the kernel is issue-bound, not HBM-bound: its measured issue-side
             # utilisation (profiled) and the measured copy ceiling
-            "issue": profiled_issue(cfg),
+            # (profiled on the single-deployment kernel only)
+            "issue": profiled_issue(cfg) if engine_id == 2 else None,
             "totals": {"cost_usd": totals.cost_uphmin / 6e7, "energy_kwh": totals.energy_wmin / 6e4,
                        "gco2_kg": totals.gco2 / 1e3, "slo_minutes": totals.slo_minutes,
                        "launches": totals.launches, "deletions": totals.deletions},
