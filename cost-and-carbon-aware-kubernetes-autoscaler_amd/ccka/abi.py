@@ -20,7 +20,7 @@ HIST = 8
 
 CAP_SPOT, CAP_OD = 1, 2
 POLICY_KEEP, WHEN_EMPTY, WHEN_EMPTY_OR_UNDERUTILIZED = 0, 1, 2
-SCALER_STATIC, SCALER_HPA, SCALER_KEDA = 0, 1, 2
+SCALER_STATIC, SCALER_HPA, SCALER_KEDA, SCALER_KEDA_TRIGGER = 0, 1, 2, 3
 PROFILE_RESET, PROFILE_OFFPEAK, PROFILE_PEAK = 0, 1, 2
 SELECT_MAX, SELECT_MIN, SELECT_DISABLED = 0, 1, 2
 HPA_PODS, HPA_PERCENT = 1, 2

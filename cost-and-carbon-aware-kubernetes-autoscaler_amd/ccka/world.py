@@ -255,6 +255,13 @@ def deployment(scaler=abi.SCALER_HPA, replicas0=5, min_r=1, max_r=100, target=70
     return d
 
 
+def keda_trigger(threshold, activation=0):
+    """An extra ScaledObject trigger of the KEDA deployment listed just before it
+    (CCKA_SCALER_KEDA_TRIGGER: owns no pods; its load column is the metric)."""
+    return deployment(abi.SCALER_KEDA_TRIGGER, replicas0=0, min_r=0, max_r=0, pdb=0,
+                      keda_threshold=threshold, keda_activation=activation)
+
+
 def burst_deployments(count=12, replicas=5):
     """demo_30_burst_configure.sh:57-151: odd -> spot, even -> on-demand, static replicas."""
     out = []

@@ -441,13 +441,17 @@ int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
   }
   for (int d = 0; d < w->n_deploy; ++d) {
     const ccka_deployment& dp = w->deploy[d];
-    if (dp.scaler < 0 || dp.scaler > 2 || dp.cap_sel == 0 || dp.cap_sel > 3 || dp.req_cpu_m < 0 ||
+    if (dp.scaler < 0 || dp.scaler > 3 || dp.cap_sel == 0 || dp.cap_sel > 3 || dp.req_cpu_m < 0 ||
         dp.req_mem_mi < 0 || dp.replicas0 < 0)
       return fail(c, CCKA_EINVAL, "deployment %d invalid", d);
     if (dp.scaler == CCKA_SCALER_HPA && (dp.req_cpu_m <= 0 || dp.target_util_pct <= 0))
       return fail(c, CCKA_EINVAL, "HPA deployment %d needs cpu request and target", d);
-    if (dp.scaler == CCKA_SCALER_KEDA && dp.keda_threshold <= 0)
+    if ((dp.scaler == CCKA_SCALER_KEDA || dp.scaler == CCKA_SCALER_KEDA_TRIGGER) && dp.keda_threshold <= 0)
       return fail(c, CCKA_EINVAL, "KEDA deployment %d needs threshold", d);
+    if (dp.scaler == CCKA_SCALER_KEDA_TRIGGER &&
+        (d == 0 || dp.replicas0 != 0 || dp.pdb_member ||
+         (w->deploy[d - 1].scaler != CCKA_SCALER_KEDA && w->deploy[d - 1].scaler != CCKA_SCALER_KEDA_TRIGGER)))
+      return fail(c, CCKA_EINVAL, "KEDA trigger %d must follow a KEDA deployment and own no pods", d);
     if (!rules_ok(dp.up) || !rules_ok(dp.down))
       return fail(c, CCKA_EINVAL, "deployment %d behavior outside the %d s history", d,
                   CCKA_HIST * CCKA_STEP_SECONDS);

@@ -539,8 +539,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     uint32_t flags = 0;
     int step_last_type = 0xFFFF;
     int util_valid[DMAX], util[DMAX], pend[DMAX];
+    bool kact_any[DMAX];
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; pend[d] = 0; }
+    for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; pend[d] = 0; kact_any[d] = false; }
 
     if (active) {
       // ---- B. readiness transitions (nominated pods start running) ----
@@ -584,7 +585,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         if (d >= D) break;
         const Dep& dp = dep[d];
         const int Lv = Lcur[d];
-        if (dp.scaler == CCKA_SCALER_STATIC) continue;
+        if (dp.scaler != CCKA_SCALER_HPA && dp.scaler != CCKA_SCALER_KEDA) continue;  // static / trigger
         const int ready = rpods[d];
         const int cur = replicas[d];
         int desired = cur, proposal = cur;
@@ -615,8 +616,17 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             }
             do_behavior = true;
           }
-        } else {  // KEDA
-          const bool act = (long long)Lv > dp.kact;
+        } else {  // KEDA: own trigger + the KEDA_TRIGGER entries right after d
+          bool act = (long long)Lv > dp.kact;
+          bool chain = true;
+#pragma unroll
+          for (int e = 0; e < DMAX; ++e) {
+            if (e > d) {
+              chain = chain && e < D && dep[e].scaler == CCKA_SCALER_KEDA_TRIGGER;
+              if (chain) act |= (long long)Lcur[e] > dep[e].kact;
+            }
+          }
+          kact_any[d] = act;
           if (act) last_active[d] = t;
           if (cur == 0) desired = act ? 1 : 0;
           else if (!act && dp.kmin == 0 && (t - last_active[d]) * CCKA_STEP_SECONDS >= dp.kcool)
@@ -630,6 +640,18 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             else {
               const double r = (double)Lv / ((double)dp.kthr * (double)cur);
               proposal = (dp.lo <= r && r <= dp.hi) ? cur : (int)ceil((double)Lv / (double)dp.kthr);
+              bool ch = true;
+#pragma unroll
+              for (int e = 0; e < DMAX; ++e) {
+                if (e > d) {
+                  ch = ch && e < D && dep[e].scaler == CCKA_SCALER_KEDA_TRIGGER;
+                  if (ch) {
+                    const double re = (double)Lcur[e] / ((double)dep[e].kthr * (double)cur);
+                    const int pe = (dp.lo <= re && re <= dp.hi) ? cur : (int)ceil((double)Lcur[e] / (double)dep[e].kthr);
+                    proposal = max(proposal, pe);
+                  }
+                }
+              }
               do_behavior = true;
             }
           }
@@ -1220,7 +1242,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         pending += replicas[d] - rpods[d];
         reps += replicas[d];
         if (dep[d].scaler == CCKA_SCALER_HPA && util_valid[d] && util[d] > slo_util) viol = true;
-        if (dep[d].scaler == CCKA_SCALER_KEDA && (long long)Lcur[d] > dep[d].kact && replicas[d] == 0) viol = true;
+        if (dep[d].scaler == CCKA_SCALER_KEDA && kact_any[d] && replicas[d] == 0) viol = true;
       }
       if (pending > 0) viol = true;
       if (viol) { slo++; flags |= 8u; }

@@ -342,22 +342,62 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
     D.up = rules_from(h->at({"spec", "behavior", "scaleUp"}), true, 0);
     D.down = rules_from(h->at({"spec", "behavior", "scaleDown"}), false, 300);
   }
-  // ---- KEDA ScaledObjects (AverageValue triggers)
+  // ---- KEDA ScaledObjects (AverageValue triggers); triggers[1..] become
+  // CCKA_SCALER_KEDA_TRIGGER entries placed right after their deployment
+  auto trig_params = [](const Value* md, int64_t* thr, int64_t* act) {
+    for (const char* k : {"value", "threshold", "targetValue", "queueLength"})
+      if (const Value* v = md->get(k)) *thr = (int64_t)std::llround(std::atof(v->as_string().c_str()));
+    for (const char* k : {"activationThreshold", "activationValue", "activationTargetValue", "activationQueueLength"})
+      if (const Value* v = md->get(k)) *act = (int64_t)std::llround(std::atof(v->as_string().c_str()));
+  };
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> extra(deps.size());
+  size_t n_extra = 0;
   for (const Value* so : store.all("ScaledObject")) {
-    ccka_deployment& D = w->deploy[dep_index(so->at({"spec", "scaleTargetRef", "name"}))];
+    const int di = dep_index(so->at({"spec", "scaleTargetRef", "name"}));
+    ccka_deployment& D = w->deploy[di];
     D.scaler = CCKA_SCALER_KEDA;
     D.keda_min = (int32_t)(so->at({"spec", "minReplicaCount"}) ? so->at({"spec", "minReplicaCount"})->as_int() : 0);
     D.keda_max = (int32_t)(so->at({"spec", "maxReplicaCount"}) ? so->at({"spec", "maxReplicaCount"})->as_int() : 100);
     D.keda_cooldown_s = (int32_t)(so->at({"spec", "cooldownPeriod"}) ? so->at({"spec", "cooldownPeriod"})->as_int() : 300);
     const Value* md = so->at({"spec", "triggers", "0", "metadata"});
     if (!md) throw ParseError("ScaledObject without triggers[0].metadata");
-    for (const char* k : {"value", "threshold", "targetValue", "queueLength"})
-      if (const Value* v = md->get(k)) D.keda_threshold = (int64_t)std::llround(std::atof(v->as_string().c_str()));
-    for (const char* k : {"activationThreshold", "activationValue", "activationTargetValue", "activationQueueLength"})
-      if (const Value* v = md->get(k)) D.keda_activation = (int64_t)std::llround(std::atof(v->as_string().c_str()));
+    trig_params(md, &D.keda_threshold, &D.keda_activation);
+    const Value* trs = so->at({"spec", "triggers"});
+    for (size_t j = 1; trs && trs->is_seq() && j < trs->seq.size(); ++j) {
+      const Value* mj = trs->seq[j].get("metadata");
+      if (!mj) throw ParseError("ScaledObject trigger without metadata");
+      int64_t thr = 0, act = 0;
+      trig_params(mj, &thr, &act);
+      extra[di].push_back({thr, act});
+      ++n_extra;
+    }
     const Value* beh = so->at({"spec", "advanced", "horizontalPodAutoscalerConfig", "behavior"});
     D.up = rules_from(beh ? beh->get("scaleUp") : nullptr, true, 0);
     D.down = rules_from(beh ? beh->get("scaleDown") : nullptr, false, 300);
+  }
+  if (n_extra) {
+    if (deps.size() + n_extra > CCKA_MAX_DEPLOY) throw ParseError("more than 16 Deployments + extra KEDA triggers");
+    std::vector<ccka_deployment> out;
+    std::vector<std::string> names;
+    for (size_t d = 0; d < deps.size(); ++d) {
+      out.push_back(w->deploy[d]);
+      names.push_back(meta.deploy_names[d]);
+      for (size_t j = 0; j < extra[d].size(); ++j) {
+        ccka_deployment T{};
+        T.scaler = CCKA_SCALER_KEDA_TRIGGER;
+        T.cap_sel = w->deploy[d].cap_sel;
+        T.tolerance = 0.1;
+        T.keda_threshold = extra[d][j].first;
+        T.keda_activation = extra[d][j].second;
+        T.up = rules_from(nullptr, true, 0);
+        T.down = rules_from(nullptr, false, 300);
+        out.push_back(T);
+        names.push_back(meta.deploy_names[d] + "/trigger-" + std::to_string(j + 1));
+      }
+    }
+    for (size_t d = 0; d < out.size(); ++d) w->deploy[d] = out[d];
+    w->n_deploy = (int32_t)out.size();
+    meta.deploy_names = names;
   }
   // ---- catalog, tiles, cluster defaults
   w->n_steps = n_steps;

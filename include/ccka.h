@@ -57,7 +57,11 @@ enum ccka_status {
 enum { CCKA_CAP_SPOT = 1, CCKA_CAP_OD = 2 };
 /* NodePool spec.disruption.consolidationPolicy */
 enum { CCKA_POLICY_KEEP = 0, CCKA_WHEN_EMPTY = 1, CCKA_WHEN_EMPTY_OR_UNDERUTILIZED = 2 };
-enum { CCKA_SCALER_STATIC = 0, CCKA_SCALER_HPA = 1, CCKA_SCALER_KEDA = 2 };
+/* CCKA_SCALER_KEDA_TRIGGER: an extra trigger of the KEDA deployment that
+ * precedes it (a chain KEDA, TRIGGER, TRIGGER...). It owns no pods; its load
+ * column is that trigger's metric and keda_threshold / keda_activation its
+ * targets (multi-trigger ScaledObject; SEMANTICS 3.C). */
+enum { CCKA_SCALER_STATIC = 0, CCKA_SCALER_HPA = 1, CCKA_SCALER_KEDA = 2, CCKA_SCALER_KEDA_TRIGGER = 3 };
 enum { CCKA_PROFILE_RESET = 0, CCKA_PROFILE_OFFPEAK = 1, CCKA_PROFILE_PEAK = 2 };
 /* HPA behavior */
 enum { CCKA_SELECT_MAX = 0, CCKA_SELECT_MIN = 1, CCKA_SELECT_DISABLED = 2 };

@@ -399,7 +399,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       st.profile = prof;
     }
     /* ---- C. scalers ---- */
-    int util_valid[CCKA_MAX_DEPLOY], util[CCKA_MAX_DEPLOY];
+    int util_valid[CCKA_MAX_DEPLOY], util[CCKA_MAX_DEPLOY], keda_act[CCKA_MAX_DEPLOY] = {0};
     int64_t Lt[CCKA_MAX_DEPLOY];
     for (int d = 0; d < D; ++d) {
       const ccka_deployment* dp = &w->deploy[d];
@@ -435,7 +435,15 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           ran = 1;
         }
       } else if (dp->scaler == CCKA_SCALER_KEDA) {
-        const int active = L > dp->keda_activation;
+        /* triggers: this deployment's own + the KEDA_TRIGGER entries after it;
+         * active if any trigger is, proposal = max over triggers (upstream HPA
+         * with several external metrics) */
+        int nt = 1;
+        while (d + nt < D && w->deploy[d + nt].scaler == CCKA_SCALER_KEDA_TRIGGER) ++nt;
+        int active = 0;
+        for (int j = 0; j < nt; ++j)
+          active |= load[((int64_t)t * D + d + j) * nl + col] > w->deploy[d + j].keda_activation;
+        keda_act[d] = active;
         if (active) ds->last_active = t;
         if (cur == 0) desired = active ? 1 : 0;
         else if (!active && dp->keda_min == 0 &&
@@ -449,13 +457,18 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           else if (cur < minr) desired = minr;
           else {
             proposal = ccka_oracle_keda_proposal(cur, L, dp->keda_threshold, dp->tolerance);
+            for (int j = 1; j < nt; ++j) {
+              const int32_t pj = ccka_oracle_keda_proposal(cur, load[((int64_t)t * D + d + j) * nl + col],
+                                                           w->deploy[d + j].keda_threshold, dp->tolerance);
+              if (pj > proposal) proposal = pj;
+            }
             desired = ccka_oracle_hpa_behavior(cur, proposal, minr, mx, &dp->up, &dp->down, ds->rec,
                                                ds->rec_valid, ds->delta);
             ran = 1;
           }
         }
       }
-      if (dp->scaler != CCKA_SCALER_STATIC) {
+      if (dp->scaler == CCKA_SCALER_HPA || dp->scaler == CCKA_SCALER_KEDA) {
         /* shift history rings: entry 0 becomes this step */
         for (int k = CCKA_HIST - 1; k > 0; --k) {
           ds->rec[k] = ds->rec[k - 1];
@@ -758,7 +771,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
         reps += st.dep[d].replicas;
         const ccka_deployment* dp = &w->deploy[d];
         if (dp->scaler == CCKA_SCALER_HPA && util_valid[d] && util[d] > w->slo_util_pct) viol = 1;
-        if (dp->scaler == CCKA_SCALER_KEDA && Lt[d] > dp->keda_activation && st.dep[d].replicas == 0) viol = 1;
+        if (dp->scaler == CCKA_SCALER_KEDA && keda_act[d] && st.dep[d].replicas == 0) viol = 1;
       }
       if (pending > 0) viol = 1;
       if (viol) { st.slo++; flags |= 8; }

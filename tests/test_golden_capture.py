@@ -254,3 +254,54 @@ spec:
     d = w.deploy[0]
     assert (d.scaler, d.keda_min, d.keda_max, d.keda_cooldown_s) == (abi.SCALER_KEDA, 0, 30, 120)
     assert (d.keda_threshold, d.keda_activation, d.cap_sel) == (50, 5, 3)
+
+
+def test_keda_multi_trigger_ingest():
+    """triggers[1..] of a ScaledObject become KEDA_TRIGGER entries right after
+    their deployment; the deployments after it shift by the trigger count."""
+    h = Host()
+    h.apply(h.manifest(-1))
+    h.apply("""apiVersion: apps/v1
+kind: Deployment
+metadata: {name: worker}
+spec:
+  replicas: 0
+  template:
+    spec:
+      nodeSelector: {karpenter.sh/capacity-type: spot}
+      containers:
+      - name: w
+        resources: {requests: {cpu: 100m, memory: 64Mi}}
+---
+apiVersion: apps/v1
+kind: Deployment
+metadata: {name: web}
+spec:
+  replicas: 2
+  template:
+    spec:
+      containers:
+      - name: w
+        resources: {requests: {cpu: 200m, memory: 128Mi}}
+---
+apiVersion: keda.sh/v1alpha1
+kind: ScaledObject
+metadata: {name: worker-so}
+spec:
+  scaleTargetRef: {name: worker}
+  triggers:
+  - type: aws-sqs-queue
+    metadata: {queueLength: "50", activationQueueLength: "5"}
+  - type: prometheus
+    metadata: {threshold: "200", activationThreshold: "20"}
+  - type: cpu
+    metadata: {value: "60"}
+""")
+    w = h.build_world("tiny", 60, 8)
+    assert w.n_deploy == 4
+    d0, t1, t2, d3 = (w.deploy[i] for i in range(4))
+    assert d0.scaler == abi.SCALER_KEDA and (d0.keda_threshold, d0.keda_activation) == (50, 5)
+    assert t1.scaler == abi.SCALER_KEDA_TRIGGER and (t1.keda_threshold, t1.keda_activation) == (200, 20)
+    assert t2.scaler == abi.SCALER_KEDA_TRIGGER and (t2.keda_threshold, t2.keda_activation) == (60, 0)
+    assert (t1.replicas0, t1.pdb_member, t1.cap_sel) == (0, 0, abi.CAP_SPOT)
+    assert d3.scaler == abi.SCALER_STATIC and d3.replicas0 == 2

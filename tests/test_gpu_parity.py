@@ -317,3 +317,39 @@ def test_drift_parity_multi_deployment(engine):
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
     assert ((tc["flags"] & 16) != 0).any()
     compare(rg, rc, tg, tc)
+
+
+# ---------------------------------------------------------------------------
+# multi-trigger KEDA ScaledObjects (SEMANTICS 3.C)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("drift", [0, 1])
+def test_keda_multi_trigger_parity(engine, drift):
+    """HPA on spot + a 3-trigger KEDA worker (own column + 2 KEDA_TRIGGER
+    columns with their own thresholds / activations) + a 2-trigger KEDA worker."""
+    from ccka.world import keda_trigger
+    spec = configs.config2_world(max_nodes=12)
+    spec.drift = drift
+    spec.deploys = [
+        deployment(abi.SCALER_HPA, cap_sel=abi.CAP_SPOT),
+        deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=900, keda_activation=2500,
+                   keda_cooldown=240, cap_sel=abi.CAP_SPOT | abi.CAP_OD, keda_max=40),
+        keda_trigger(1200, 3000),
+        keda_trigger(2500, 6000),
+        deployment(abi.SCALER_KEDA, replicas0=1, keda_threshold=1500, keda_activation=1000,
+                   keda_cooldown=300, keda_min=1, keda_max=20, req_cpu=300, cap_sel=abi.CAP_OD),
+        keda_trigger(700, 4000),
+    ]
+    n = 600
+    sc = ScenarioSet(n)
+    load = po.gen_load(configs.trace_gen(13), spec.n_steps, len(spec.deploys), n)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
+
+
+def test_keda_trigger_validation(engine):
+    from ccka.world import keda_trigger
+    spec = configs.config2_world(n_steps=60)
+    spec.deploys = [deployment(abi.SCALER_HPA), keda_trigger(500)]  # trigger after an HPA
+    with pytest.raises(abi.CckaError):
+        engine.set_world(spec)

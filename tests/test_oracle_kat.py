@@ -327,3 +327,31 @@ def test_drift_blocked_by_pdb_and_budget():
         p.budget_pct = 0
     r, _ = run(spec, np.zeros((30, 1, 1), np.int32))
     assert r["deletions"][0] == 0 and r["launches"][0] == 1
+
+
+# ---------------------------------------------------------------- multi-trigger KEDA (SEMANTICS §3.C)
+def test_keda_multi_trigger_any_active_max_proposal():
+    """Trigger 0 (own column) never fires; trigger 1 (threshold 500,
+    activation 100) carries 1500 for 10 steps: active via trigger 1, 0 -> 1 at
+    t=0, then max(ceil(0/1000)=0, ceil(1500/500)=3) = 3; idle from t=10, back
+    to 0 once 60*(t-9) >= 300. Without the trigger nothing ever activates."""
+    from ccka.world import keda_trigger
+    d = deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=1000, keda_activation=0,
+                   keda_cooldown=300, keda_min=0, keda_max=10)
+    spec = tiny_world([d, keda_trigger(500, 100)], T=30, peak_switch=0)
+    load = np.zeros((30, 2, 1), np.int32)
+    load[:10, 1] = 1500
+    r, tr = run(spec, load)
+    reps = tr["replicas"][:, 0]
+    assert reps[0] == 1 and reps[1] == 3 and reps[9] == 3
+    assert reps[13] > 0 and reps[14] == 0
+    assert r["launches"][0] >= 1
+    # the trigger alone decides: drop it and the deployment stays at zero
+    spec1 = tiny_world([d], T=30, peak_switch=0)
+    r1, tr1 = run(spec1, np.ascontiguousarray(load[:, :1]))
+    assert (tr1["replicas"][:, 0] == 0).all() and r1["launches"][0] == 0
+    # both triggers active: the larger proposal wins (own: ceil(4000/1000) = 4)
+    load2 = load.copy()
+    load2[:10, 0] = 4000
+    _, tr2 = run(spec, load2)
+    assert tr2["replicas"][1, 0] == 4
