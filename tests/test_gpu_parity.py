@@ -278,7 +278,8 @@ def test_d1_matches_general_kernel(engine):
 # ---------------------------------------------------------------------------
 # Karpenter drift on the peak/off-peak zone switch (SEMANTICS 3.G0)
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("variant", ["pdb50", "no_pdb", "budget50", "wrap_peak"])
+@pytest.mark.parametrize("variant", ["pdb50", "no_pdb", "budget50", "wrap_peak", "pool_limit", "delay0",
+                                     "delay3", "one_slot", "slots16"])
 def test_drift_parity_single_deployment(engine, variant):
     spec = configs.config2_world(n_steps=1440)
     spec.drift = 1
@@ -291,6 +292,18 @@ def test_drift_parity_single_deployment(engine, variant):
             p.budget_pct = 50
     elif variant == "wrap_peak":
         spec.peak_start, spec.peak_end, spec.start_minute = 1300, 200, 1200
+        spec.pdb_pct = -1
+    elif variant == "pool_limit":
+        for p in spec.pools:
+            p.limit_cpu_m = 12000
+    elif variant in ("delay0", "delay3"):
+        spec.provision_delay_steps = int(variant[-1])
+        spec.pdb_pct = -1
+    elif variant == "one_slot":
+        spec.max_nodes = 1
+        spec.pdb_pct = -1
+    elif variant == "slots16":
+        spec.max_nodes = 16
         spec.pdb_pct = -1
     load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=sc.first_id)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
