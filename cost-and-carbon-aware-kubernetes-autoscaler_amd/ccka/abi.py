@@ -21,6 +21,7 @@ HIST = 8
 CAP_SPOT, CAP_OD = 1, 2
 POLICY_KEEP, WHEN_EMPTY, WHEN_EMPTY_OR_UNDERUTILIZED = 0, 1, 2
 SCALER_STATIC, SCALER_HPA, SCALER_KEDA, SCALER_KEDA_TRIGGER = 0, 1, 2, 3
+DISRUPT_DRIFT, DISRUPT_REPLACE = 1, 2
 PROFILE_RESET, PROFILE_OFFPEAK, PROFILE_PEAK = 0, 1, 2
 SELECT_MAX, SELECT_MIN, SELECT_DISABLED = 0, 1, 2
 HPA_PODS, HPA_PERCENT = 1, 2
@@ -77,7 +78,7 @@ class World(C.Structure):
                 ("base_util", C.c_double), ("carbon_weight", C.c_double),
                 ("pdb_min_available_pct", C.c_int32), ("peak_start_min", C.c_int32),
                 ("peak_end_min", C.c_int32), ("peak_switch", C.c_int32),
-                ("reset_ca_s", C.c_int32), ("drift", C.c_int32)]
+                ("reset_ca_s", C.c_int32), ("disrupt_ext", C.c_int32)]
 
 
 class Scenarios(C.Structure):

@@ -293,7 +293,8 @@ class WorldSpec:
     peak_switch: int = 1
     reset_ca_s: int = 30
     carbon_weight: float = 0.0
-    drift: int = 0
+    drift: int = 0                 # CCKA_DISRUPT_DRIFT
+    replace: int = 0               # CCKA_DISRUPT_REPLACE
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -339,7 +340,7 @@ class WorldSpec:
         w.peak_end_min = self.peak_end
         w.peak_switch = self.peak_switch
         w.reset_ca_s = self.reset_ca_s
-        w.drift = self.drift
+        w.disrupt_ext = (abi.DISRUPT_DRIFT if self.drift else 0) | (abi.DISRUPT_REPLACE if self.replace else 0)
         return w
 
 

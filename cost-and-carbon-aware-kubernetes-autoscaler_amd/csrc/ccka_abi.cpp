@@ -204,7 +204,7 @@ static int d1_check_world(ccka_ctx* c) {
   c->d1_ready = false;
   const ccka_deployment& dp = w.deploy[0];
   if (w.n_deploy != 1 || dp.scaler != CCKA_SCALER_HPA) return CCKA_OK;
-  if (w.drift) return CCKA_OK;  // drift disruption runs on the general kernel
+  if (w.disrupt_ext) return CCKA_OK;  // drift / replacement run on the general kernel
   for (int q = 0; q < w.n_pools; ++q)
     if (w.pools[q].limit_cpu_m >= 0) return CCKA_OK;
   if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
@@ -431,7 +431,8 @@ int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
   if (w->n_pools < 1 || w->n_pools > CCKA_MAX_POOLS) return fail(c, CCKA_EINVAL, "n_pools out of range");
   if (w->n_deploy < 1 || w->n_deploy > CCKA_MAX_DEPLOY) return fail(c, CCKA_EINVAL, "n_deploy out of range");
   if (!w->price_uph || !w->ci_gpwh || !w->ci_gpwmin) return fail(c, CCKA_EINVAL, "tiles missing");
-  if (w->drift != 0 && w->drift != 1) return fail(c, CCKA_EINVAL, "drift must be 0 or 1");
+  if (w->disrupt_ext & ~(CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE))
+    return fail(c, CCKA_EINVAL, "unknown disrupt_ext bits");
   if (w->base_type < 0 || w->base_type >= w->n_types) return fail(c, CCKA_EINVAL, "base_type out of range");
   if (w->provision_delay_steps < 0 || w->start_minute < 0) return fail(c, CCKA_EINVAL, "negative timing");
   for (int k = 0; k < w->n_types; ++k) {

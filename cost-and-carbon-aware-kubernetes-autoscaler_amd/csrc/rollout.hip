@@ -396,7 +396,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     plimit[q] = gw->pools[q].limit_cpu_m;
   }
   const int pdb_pct = gw->pdb_min_available_pct;
-  const bool gdrift = gw->drift != 0;
+  const bool gdrift = (gw->disrupt_ext & CCKA_DISRUPT_DRIFT) != 0;
+  const bool greplace = (gw->disrupt_ext & CCKA_DISRUPT_REPLACE) != 0;
   const int slo_util = gw->slo_util_pct;
   const int base_nodes = gw->base_nodes, base_type = gw->base_type;
 
@@ -452,11 +453,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   // node slots; `used` / `rdy` are bitmasks over slots. nprice caches the
   // slot's offering price for the current hour, ncap (D == 1) its pod capacity.
   uint32_t ninfo[MAXN];
+  int nsrc[MAXN];  // replacement node: 1 + the slot it replaces (SEMANTICS 3.G2)
   int nready[MAXN], nlast[MAXN], nprice[MAXN], ncap[MAXN];
   int npods[MAXN][DMAX];
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
-    ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+    ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
   }
@@ -527,6 +529,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         ci_gpwh = s_ci[(rl * 24 + h) * 2 + 1];
         base_price = (long long)base_nodes * tprice(L, rl, base_type, 0, 1);
         burn = 0;
+        if (greplace) g_dirty = true;  // replacement offers depend on this hour's prices
 #pragma unroll
         for (int n = 0; n < MAXN; ++n) {
           if (used >> n & 1u) {
@@ -907,6 +910,182 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           }
           allowed = max(rdyp - ((long long)pdb_pct * reps + 99) / 100, 0LL);
         }
+        // a freed slot's pending replacement becomes an ordinary node
+        auto unlink = [&](int b) {
+#pragma unroll
+          for (int m = 0; m < MAXN; ++m) if (nsrc[m] == b + 1) nsrc[m] = 0;
+        };
+        auto free_slot = [&](int b) {
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (n == b) {
+              if (ni_cap(ninfo[n]) == 0) nsp--; else nod--;
+#pragma unroll
+              for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+                if (qq == ni_pool(ninfo[n])) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
+              burn -= nprice[n];
+              ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
+            }
+          }
+          used &= ~(1u << b);
+          rdy &= ~(1u << b);
+          unlink(b);
+        };
+        // ---- G2. single-node replacement consolidation (SEMANTICS 3.G2): the
+        // first candidate in (pods asc, price desc, slot asc) order that is
+        // on-demand, has pods, is not being replaced and has a strictly cheaper
+        // single offering gets a pre-spun replacement; one per pool per step
+        auto try_replace = [&](int q, int qca, int budget, int& deleted) {
+          uint32_t srcm = 0, pq = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (nsrc[n]) srcm |= 1u << (nsrc[n] - 1);
+            pq |= (ni_pool(ninfo[n]) == q && ni_cap(ninfo[n]) == 1 ? 1u : 0u) << n;
+          }
+          uint32_t cand = rdy & pq & ~srcm;
+          while (deleted < budget) {
+            int best = -1, bpods = 0, bprice = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (!(cand >> n & 1u)) continue;
+              if ((t - nlast[n]) * CCKA_STEP_SECONDS < qca) continue;
+              int pods = 0;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n][d] : 0;
+              if (pods == 0) continue;
+              const int pr = nprice[n];
+              if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
+            }
+            if (best < 0) break;
+            const uint32_t fr = ~used & slot_mask;
+            if (!fr) break;
+            const int slot = __builtin_ctz(fr);
+            long long pdb_pods = 0;
+            int s_cpu = 0, s_mem = 0, s_pods = 0;
+            uint32_t cm = 0, zm = 0;
+            int use = 0, limit = 0;
+#pragma unroll
+            for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+              if (qq == q) { cm = pcm[qq]; zm = pzm[qq]; use = puse[qq]; limit = plimit[qq]; }
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) {
+              int bp = 0;
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) if (n == best) bp = npods[n][d];
+              if (d >= D || bp <= 0) continue;
+              if (dep[d].pdb) pdb_pods += bp;
+              cm &= capsel[d];
+              s_cpu += bp * dep[d].req_cpu;
+              s_mem += bp * dep[d].req_mem;
+              s_pods += bp;
+            }
+            cand &= ~(1u << best);
+            if (pdb_pods > allowed || !cm) continue;
+            int bk = -1, bz = 0, bc = 0, bpr = 0;
+            for (int k = 0; k < L.K; ++k) {
+              if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
+              if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+              for (int z = 0; z < L.Z; ++z) {
+                if (!(zm >> z & 1u)) continue;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                  if (!(cm & capbit(c))) continue;
+                  const int pr = tprice(L, rl, k, z, c);
+                  if (pr > 0 && (bk < 0 || pr < bpr)) { bk = k; bz = z; bc = c; bpr = pr; }
+                }
+              }
+            }
+            if (bk < 0 || bpr >= bprice) continue;
+            const bool now_ready = delay == 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (n == slot) {
+                ninfo[n] = ni_make(q, bk, bz, bc);
+                nready[n] = t + delay;
+                nlast[n] = t;
+                nprice[n] = bpr;
+                ncap[n] = DMAX == 1 ? L.cap1[bk] : 0;
+                nsrc[n] = best + 1;
+#pragma unroll
+                for (int e = 0; e < DMAX; ++e) npods[n][e] = 0;
+              }
+            }
+            used |= 1u << slot;
+            if (now_ready) rdy |= 1u << slot;
+            else next_ready = min(next_ready, t + delay);
+#pragma unroll
+            for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq) if (qq == q) puse[qq] += L.types[bk].vcpu * 1000;
+            if (bc == 0) nsp++; else nod++;
+            burn += bpr;
+            launches++;
+            last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+            hash = (hash ^ last_choice) * 16777619u;
+            step_last_type = bk;
+            flags |= 2u | 32u;
+            deleted++;
+            break;
+          }
+        };
+        // ---- G1. ready replacements take over their source's pods (SEMANTICS 3.G2) ----
+        if (greplace) {
+          uint32_t rm = 0;
+#pragma unroll
+          for (int m = 0; m < MAXN; ++m) rm |= ((nsrc[m] != 0) && (rdy >> m & 1u) ? 1u : 0u) << m;
+          while (rm) {
+            const int m = __builtin_ctz(rm);
+            rm &= rm - 1u;
+            int src = 0;
+            uint32_t xm = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) if (n == m) { src = nsrc[n] - 1; nsrc[n] = 0; xm = ninfo[n]; }
+            int sp[DMAX];
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) {
+              sp[d] = 0;
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) if (n == src) sp[d] = npods[n][d];
+            }
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) {
+              if (d >= D) break;
+              int k = 0;
+              if (capbit(ni_cap(xm)) & capsel[d]) {
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) {
+                  if (n == m) {
+                    int f;
+                    if (DMAX == 1) {
+                      f = ncap[n] - npods[n][0];
+                    } else {
+                      int sc = 0, sm = 0, spp = 0;
+#pragma unroll
+                      for (int e = 0; e < DMAX; ++e) {
+                        if (e >= D) break;
+                        sc += npods[n][e] * dep[e].req_cpu;
+                        sm += npods[n][e] * dep[e].req_mem;
+                        spp += npods[n][e];
+                      }
+                      f = max(type_fit<DMAX>(L, ni_type(xm), sc, sm, spp, dep[d].req_cpu, dep[d].req_mem), 0);
+                    }
+                    k = min(f, sp[d]);
+                    npods[n][d] += k;
+                  }
+                }
+              }
+              rpods[d] -= sp[d] - k;
+              placed[d] -= sp[d] - k;
+            }
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) if (n == m) nlast[n] = t;
+            free_slot(src);
+            rm &= ~(1u << src);
+            deletions++;
+            any_deleted = true;
+            flags |= 4u;
+          }
+        }
         // drifted nodes (SEMANTICS 3.G0): zone / capacity type outside the
         // pool's current requirements
         uint32_t dmask = 0;
@@ -991,13 +1170,14 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
                   for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
                     if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
-                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
 #pragma unroll
                   for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
                 }
               }
               burn -= bprice;
               used &= ~(1u << best);
+              unlink(best);
               rdy &= ~(1u << best);
               dmask &= ~(1u << best);
               allowed -= pdb_pods;
@@ -1058,12 +1238,13 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
                   for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
                     if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
-                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
                   npods[n][0] = 0;
                 }
               }
               burn -= bprice;
               used &= ~(1u << best);
+              unlink(best);
               rdy &= ~(1u << best);
               pm &= ~(1u << best);
               cm1 &= ~(1u << best);
@@ -1073,6 +1254,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               any_deleted = true;
               flags |= 4u;
             }
+            if (greplace && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
             continue;
           }
           uint32_t rejected = 0;
@@ -1175,13 +1357,14 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
                 for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
                   if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
-                ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0;
+                ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
 #pragma unroll
                 for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
               }
             }
             burn -= bprice;
             used &= ~(1u << best);
+              unlink(best);
             rdy &= ~(1u << best);
             allowed -= pdb_pods;
             deleted++;
@@ -1189,8 +1372,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             any_deleted = true;
             flags |= 4u;
           }
+          if (greplace && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
         }
-        g_dirty = budget_hit || any_deleted || dmask != 0;
+        bool pending_repl = false;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) pending_repl |= nsrc[n] != 0;
+        g_dirty = budget_hit || any_deleted || dmask != 0 || pending_repl;
         // next step at which a node becomes a new candidate (consolidatable and ready)
         int wake = 0x7fffffff;
 #pragma unroll

@@ -168,7 +168,7 @@ int main(int argc, char** argv) {
   }
   ccka_world w;
   if (ccka_host_build_world(h, catalog.c_str(), steps, max_nodes, &w) != CCKA_OK) die_host(h, "build world");
-  w.drift = drift;  // Karpenter drift on the zone switch (SEMANTICS 3.G0)
+  w.disrupt_ext = drift ? CCKA_DISRUPT_DRIFT : 0;  // Karpenter drift on the zone switch (SEMANTICS 3.G0)
 
   // decisions: one cluster on the GPU
   ccka_ctx* ctx = nullptr;

@@ -420,7 +420,7 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
   w->peak_end_min = 1260;
   w->peak_switch = 1;
   w->reset_ca_s = 30;
-  w->drift = 0;  // opt-in (ccka replay --drift)
+  w->disrupt_ext = 0;  // opt-in (ccka replay --drift)
   return meta;
 }
 

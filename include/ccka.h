@@ -61,6 +61,10 @@ enum { CCKA_POLICY_KEEP = 0, CCKA_WHEN_EMPTY = 1, CCKA_WHEN_EMPTY_OR_UNDERUTILIZ
  * precedes it (a chain KEDA, TRIGGER, TRIGGER...). It owns no pods; its load
  * column is that trigger's metric and keda_threshold / keda_activation its
  * targets (multi-trigger ScaledObject; SEMANTICS 3.C). */
+/* ccka_world.disrupt_ext */
+#define CCKA_DISRUPT_DRIFT 1    /* drift on a zone / capacity-type requirement change */
+#define CCKA_DISRUPT_REPLACE 2  /* single-node replacement consolidation (on-demand ->
+                                   strictly cheaper offering, pre-spun replacement) */
 enum { CCKA_SCALER_STATIC = 0, CCKA_SCALER_HPA = 1, CCKA_SCALER_KEDA = 2, CCKA_SCALER_KEDA_TRIGGER = 3 };
 enum { CCKA_PROFILE_RESET = 0, CCKA_PROFILE_OFFPEAK = 1, CCKA_PROFILE_PEAK = 2 };
 /* HPA behavior */
@@ -163,9 +167,9 @@ typedef struct ccka_world {
   int32_t peak_end_min;
   int32_t peak_switch;          /* 1: peak/off-peak switch on            */
   int32_t reset_ca_s;           /* consolidateAfter of the RESET profile */
-  int32_t drift;                /* 1: Karpenter drift disruption on a zone /
-                                   capacity-type requirement change
-                                   (docs/SEMANTICS.md 3.G0) */
+  int32_t disrupt_ext;          /* CCKA_DISRUPT_* bits: Karpenter disruption
+                                   beyond WhenEmpty / WhenEmptyOrUnderutilized
+                                   deletes (SEMANTICS 3.G0, 3.G2) */
 } ccka_world;
 
 /* Per-scenario parameters, SoA, host pointers. NULL ⇒ world default. */

@@ -207,6 +207,7 @@ int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, i
 /* ------------------------------------------------------------------------ */
 typedef struct {
   int used, pool, type, zone, cap, ready_step, last_event;
+  int src1;  /* replacement node: 1 + the slot it replaces (0: none) */
   int pods[CCKA_MAX_DEPLOY];
 } o_node;
 
@@ -326,6 +327,13 @@ typedef struct {
 
 /* Karpenter drift: the node's zone or capacity type no longer satisfies its
  * pool's (patched) requirements. */
+/* free a slot; a pending replacement of it becomes an ordinary node */
+static void o_free(o_node* nodes, int NN, int n) {
+  memset(&nodes[n], 0, sizeof(o_node));
+  for (int m = 0; m < NN; ++m)
+    if (nodes[m].src1 == n + 1) nodes[m].src1 = 0;
+}
+
 static int o_drifted(const o_state* st, const o_node* nd) {
   const o_pool* pl = &st->pools[nd->pool];
   return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
@@ -635,6 +643,25 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     }
     /* ---- G. disruption ---- */
     {
+      /* G1. replacements that are ready take over their source node's pods
+       * (docs/SEMANTICS.md 3.G2), slot order; pods that no longer fit are
+       * evicted; the source is deleted */
+      for (int m = 0; (w->disrupt_ext & CCKA_DISRUPT_REPLACE) && m < NN; ++m) {
+        o_node* rn = &st.nodes[m];
+        if (!rn->used || !rn->src1 || rn->ready_step > t) continue;
+        const int n = rn->src1 - 1;
+        rn->src1 = 0;
+        for (int d = 0; d < D; ++d) {
+          if (!((uint32_t)o_capidx_bit(rn->cap) & capsel[d])) continue;
+          const int64_t f = o_node_fit(e, rn, d);
+          const int k = (int)(f < st.nodes[n].pods[d] ? f : st.nodes[n].pods[d]);
+          if (k > 0) rn->pods[d] += k;
+        }
+        rn->last_event = t;
+        o_free(st.nodes, NN, n);
+        st.deletions++;
+        flags |= 4;
+      }
       int64_t allowed = O_BIG;
       if (w->pdb_min_available_pct >= 0) {
         int64_t rdy = 0, reps = 0;
@@ -658,7 +685,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
          * capacity type left the pool's requirements after the patch of
          * demo_20_offpeak_configure.sh:64-81 / demo_21_peak_configure.sh:60-77,
          * slot order, sharing this pool's budget; no consolidateAfter wait */
-        for (int n = 0; w->drift && n < NN && deleted < budget; ++n) {
+        for (int n = 0; (w->disrupt_ext & CCKA_DISRUPT_DRIFT) && n < NN && deleted < budget; ++n) {
           o_node* dn = &st.nodes[n];
           if (!dn->used || dn->pool != p || dn->ready_step > t || !o_drifted(&st, dn)) continue;
           int64_t pdb_pods = 0;
@@ -677,7 +704,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
               if (k > 0) { nd->pods[d] += k; need -= k; nd->last_event = t; }
             }
           }
-          memset(dn, 0, sizeof(o_node));
+          o_free(st.nodes, NN, n);
           allowed -= pdb_pods;
           deleted++;
           st.deletions++;
@@ -722,11 +749,87 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           }
           if (!ok) { rejected[best] = 1; continue; }
           memcpy(st.nodes, trial, sizeof(o_node) * (size_t)NN);
-          memset(&st.nodes[best], 0, sizeof(o_node));
+          o_free(st.nodes, NN, best);
           allowed -= pdb_pods;
           deleted++;
           st.deletions++;
           flags |= 4;
+        }
+        /* G2. single-node replacement consolidation (docs/SEMANTICS.md 3.G2):
+         * the first candidate (same order, on-demand, with pods, not already
+         * being replaced) that has a strictly cheaper single offering for its
+         * pods gets a pre-spun replacement; one per pool per step */
+        int rej2[CCKA_MAX_NODES] = {0};
+        while ((w->disrupt_ext & CCKA_DISRUPT_REPLACE) &&
+               st.pools[p].policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED && deleted < budget) {
+          int best = -1, bpods = 0;
+          int32_t bprice = 0;
+          for (int n = 0; n < NN; ++n) {
+            const o_node* nd = &st.nodes[n];
+            if (!nd->used || nd->pool != p || nd->ready_step > t || rej2[n] || nd->cap != 1) continue;
+            if ((int64_t)(t - nd->last_event) * CCKA_STEP_SECONDS < st.pools[p].ca_s) continue;
+            int src = 0;
+            for (int m = 0; m < NN; ++m) src |= st.nodes[m].src1 == n + 1;
+            if (src) continue;
+            int pods = 0;
+            for (int d = 0; d < D; ++d) pods += nd->pods[d];
+            if (pods == 0) continue;
+            const int32_t pr = o_price(e, r, h, nd->type, nd->zone, nd->cap);
+            if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
+          }
+          if (best < 0) break;
+          int slot = -1;
+          for (int n = 0; n < NN; ++n) if (!st.nodes[n].used) { slot = n; break; }
+          if (slot < 0) break;
+          const o_node* cn = &st.nodes[best];
+          int64_t pdb_pods = 0, s_cpu = 0, s_mem = 0, s_pods = 0;
+          uint32_t cm = st.pools[p].cap_mask;
+          for (int d = 0; d < D; ++d) {
+            if (cn->pods[d] <= 0) continue;
+            if (w->deploy[d].pdb_member) pdb_pods += cn->pods[d];
+            cm &= capsel[d];
+            s_cpu += (int64_t)cn->pods[d] * w->deploy[d].req_cpu_m;
+            s_mem += (int64_t)cn->pods[d] * w->deploy[d].req_mem_mi;
+            s_pods += cn->pods[d];
+          }
+          if (pdb_pods > allowed || !cm) { rej2[best] = 1; continue; }
+          int64_t use = 0;
+          for (int n = 0; n < NN; ++n)
+            if (st.nodes[n].used && st.nodes[n].pool == p) use += (int64_t)w->types[st.nodes[n].type].vcpu * 1000;
+          const int32_t limit = w->pools[p].limit_cpu_m;
+          int bk = -1, bz = 0, bc = 0;
+          int32_t bp = 0;
+          for (int k = 0; k < K; ++k) {
+            const ccka_itype* ty = &w->types[k];
+            if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
+            if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+            for (int z = 0; z < e->Z; ++z) {
+              if (!(st.pools[p].zone_mask >> z & 1u)) continue;
+              for (int cc = 0; cc < 2; ++cc) {
+                if (!(cm & (uint32_t)o_capidx_bit(cc))) continue;
+                const int32_t pr = o_price(e, r, h, k, z, cc);
+                if (pr > 0 && (bk < 0 || pr < bp)) { bk = k; bz = z; bc = cc; bp = pr; }
+              }
+            }
+          }
+          if (bk < 0 || bp >= bprice) { rej2[best] = 1; continue; }
+          o_node* nd = &st.nodes[slot];
+          memset(nd, 0, sizeof *nd);
+          nd->used = 1;
+          nd->pool = p;
+          nd->type = bk;
+          nd->zone = bz;
+          nd->cap = bc;
+          nd->ready_step = t + w->provision_delay_steps;
+          nd->last_event = t;
+          nd->src1 = best + 1;
+          st.launches++;
+          st.last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)p << 16;
+          st.hash = (st.hash ^ st.last_choice) * 16777619u;
+          step_last_type = (uint16_t)bk;
+          flags |= 2 | 32;
+          deleted++;
+          break;
         }
       }
     }

@@ -32,7 +32,7 @@ def test_cli_replay_matches_oracle(tmp_path, load_m, catalog, drift):
         h.apply(h.manifest(i))
     h.apply(h.manifest(0))
     w = h.build_world(catalog, 1440, 16)
-    w.drift = drift
+    w.disrupt_ext = drift
     load = np.full((1440, 12, 1), load_m, np.int32)
     want, _ = po.rollout_world(w, ScenarioSet(1), load)
     for f in INT_FIELDS:

@@ -366,3 +366,58 @@ def test_keda_trigger_validation(engine):
     spec.deploys = [deployment(abi.SCALER_HPA), keda_trigger(500)]  # trigger after an HPA
     with pytest.raises(abi.CckaError):
         engine.set_world(spec)
+
+
+# ---------------------------------------------------------------------------
+# single-node replacement consolidation (SEMANTICS 3.G2)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("variant", ["spot_pool_only", "od_pool_weou", "drift_replace", "pdb50", "delay0",
+                                     "pool_limit"])
+def test_replacement_parity_single_deployment(engine, variant):
+    spec = configs.config2_world(n_steps=1440)
+    spec.replace = 1
+    spec.pdb_pct = -1
+    spec.deploys[0].cap_sel = abi.CAP_OD  # on-demand nodes in a WhenEmptyOrUnderutilized pool
+    n = 1537
+    sc = configs.hpa_scenarios(n, first_id=901)
+    if variant == "spot_pool_only":
+        spec.pools = [spec.pools[1]]
+    else:
+        spec.pools[0].profile[abi.PROFILE_OFFPEAK].policy = abi.WHEN_EMPTY_OR_UNDERUTILIZED
+    if variant == "drift_replace":
+        spec.drift = 1
+    elif variant == "pdb50":
+        spec.pdb_pct = 50
+    elif variant == "delay0":
+        spec.provision_delay_steps = 0
+    elif variant == "pool_limit":
+        for p in spec.pools:
+            p.limit_cpu_m = 12000
+    load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=sc.first_id)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 1
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    if variant != "pdb50":
+        assert ((tc["flags"] & 32) != 0).any()  # replacements happened
+    compare(rg, rc, tg, tc)
+
+
+def test_replacement_parity_multi_deployment(engine):
+    spec = configs.config2_world(max_nodes=12)
+    spec.replace = 1
+    spec.drift = 1
+    spec.pdb_pct = -1
+    spec.pools[0].profile[abi.PROFILE_OFFPEAK].policy = abi.WHEN_EMPTY_OR_UNDERUTILIZED
+    spec.deploys = [
+        deployment(abi.SCALER_HPA, cap_sel=abi.CAP_OD),
+        deployment(abi.SCALER_HPA, req_cpu=500, req_mem=512, limit_cpu=1000, cap_sel=abi.CAP_OD, target=60),
+        deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=800, keda_activation=1500,
+                   keda_cooldown=300, cap_sel=abi.CAP_SPOT | abi.CAP_OD),
+    ]
+    n = 700
+    sc = ScenarioSet(n)
+    load = po.gen_load(configs.trace_gen(9), spec.n_steps, 3, n)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert ((tc["flags"] & 32) != 0).any()
+    compare(rg, rc, tg, tc)

@@ -355,3 +355,42 @@ def test_keda_multi_trigger_any_active_max_proposal():
     load2[:10, 0] = 4000
     _, tr2 = run(spec, load2)
     assert tr2["replicas"][1, 0] == 4
+
+
+# ---------------------------------------------------------------- replacement consolidation (SEMANTICS §3.G2)
+def test_replacement_consolidation_on_demand_to_cheaper():
+    """Spot pool only (WhenEmptyOrUnderutilized off-peak), 5 on-demand pods.
+    Hour 0 offers only 8-vCPU on-demand types, so an 8-vCPU node launches at
+    t=0. From minute 60 smaller types are back: the node cannot be deleted
+    (no other node) but a strictly cheaper single offering exists, so a
+    replacement launches at t=60, takes the pods when ready at t=61 and the
+    8-vCPU node is deleted. Pods never go Pending after t=0."""
+    d = deployment(abi.SCALER_STATIC, replicas0=5, min_r=5, max_r=5, cap_sel=abi.CAP_OD)
+    spec = tiny_world([d], T=90, peak_switch=0, replace=1, pdb_pct=-1)
+    spec.pools = [reference_pools()[1]]
+    v = spec.catalog.vcpu
+    spec.price[0, 0, :, :, 1] = np.where(v[:, None] == 8, spec.price[0, 0, :, :, 1], 0)
+    load = np.zeros((90, 1, 1), np.int32)
+    r, tr = run(spec, load)
+    n = tr["nodes_od"][:, 0].astype(int) + tr["nodes_spot"][:, 0]
+    assert r["launches"][0] == 2 and r["deletions"][0] == 1
+    assert tr["flags"][60, 0] & 32 and not (tr["flags"][:60, 0] & 32).any()
+    assert n[59] == 1 and n[60] == 2 and n[61] == 1 and n[89] == 1
+    assert (tr["pending"][1:, 0] == 0).all()
+    k_new = r["last_choice"][0] & 0xFFF
+    assert v[k_new] < 8
+    spec.replace = 0
+    r0, _ = run(spec, load)
+    assert r0["launches"][0] == 1 and r0["deletions"][0] == 0
+    assert r["cost_uphmin"][0] < r0["cost_uphmin"][0]
+    # a 50 % PDB allows 2 of the 5 evictions: no replacement
+    spec.replace, spec.pdb_pct = 1, 50
+    r1, _ = run(spec, load)
+    assert r1["launches"][0] == 1 and r1["deletions"][0] == 0
+    spec.pdb_pct = -1
+    # spot nodes are never replaced (no spot-to-spot single-node replacement)
+    spec.replace = 1
+    spec.deploys = [deployment(abi.SCALER_STATIC, replicas0=5, min_r=5, max_r=5, cap_sel=abi.CAP_SPOT)]
+    spec.price[0, 0, :, :, 0] = np.where(v[:, None] == 8, spec.price[0, 0, :, :, 0], 0)
+    r2, _ = run(spec, load)
+    assert r2["launches"][0] == 1 and r2["deletions"][0] == 0
