@@ -43,7 +43,7 @@ static int usage() {
                "       ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]...\n"
                "                   [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]\n"
                "                   [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]\n"
-               "                   [--drift] [--kyverno]\n");
+               "                   [--drift] [--replace] [--kyverno]\n");
   return 2;
 }
 
@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
   long long start_ms = 0;
   std::vector<std::string> applies;
   std::vector<std::vector<std::string>> patches;
-  int steps = 1440, max_nodes = 16, device = 0, drift = 0, kyverno = 0;
+  int steps = 1440, max_nodes = 16, device = 0, drift = 0, replace = 0, kyverno = 0;
   long load_m = 100;
   for (int a = 2; a < argc; ++a) {
     auto next = [&]() -> std::string {
@@ -137,6 +137,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[a], "--csv")) csv_out = next();
     else if (!std::strcmp(argv[a], "--start-unix-ms")) start_ms = std::atoll(next().c_str());
     else if (!std::strcmp(argv[a], "--drift")) drift = 1;
+    else if (!std::strcmp(argv[a], "--replace")) replace = 1;
     else if (!std::strcmp(argv[a], "--kyverno")) kyverno = 1;
     else return usage();
   }
@@ -168,7 +169,8 @@ int main(int argc, char** argv) {
   }
   ccka_world w;
   if (ccka_host_build_world(h, catalog.c_str(), steps, max_nodes, &w) != CCKA_OK) die_host(h, "build world");
-  w.disrupt_ext = drift ? CCKA_DISRUPT_DRIFT : 0;  // Karpenter drift on the zone switch (SEMANTICS 3.G0)
+  // Karpenter drift on the zone switch / replacement consolidation (SEMANTICS 3.G0, 3.G2)
+  w.disrupt_ext = (drift ? CCKA_DISRUPT_DRIFT : 0) | (replace ? CCKA_DISRUPT_REPLACE : 0);
 
   // decisions: one cluster on the GPU
   ccka_ctx* ctx = nullptr;
