@@ -16,13 +16,15 @@ from parity import INT_FIELDS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("load_m,catalog,drift", [(100, "tiny", 0), (450, "small", 0), (450, "small", 1)])
+@pytest.mark.parametrize("load_m,catalog,drift", [(100, "tiny", 0), (450, "small", 0), (450, "small", 1),
+                                                            (450, "small", 3)])
 def test_cli_replay_matches_oracle(tmp_path, load_m, catalog, drift):
     out = tmp_path / "r.json"
     env = {k: v for k, v in os.environ.items() if k not in ("COUNT", "REPLICAS", "NP_SPOT", "NP_OD")}
     prom = tmp_path / "r.prom"
     txt = subprocess.run([CLI, "replay", "--catalog", catalog, "--load-m", str(load_m), "--json", str(out),
-                          "--prom", str(prom)] + (["--drift"] if drift else []),
+                          "--prom", str(prom)] + (["--drift"] if drift & 1 else [])
+                         + (["--replace"] if drift & 2 else []),
                          env=env, check=True, capture_output=True, text=True, timeout=120).stdout
     assert "cost=$" in txt and "spot-preferred" in txt
     got = json.load(open(out))
