@@ -73,6 +73,8 @@ struct ccka_ctx {
   bool d1_ready = false;     // scenario-dependent part prepared
   bool d1_ok = false;        // world + scenarios qualify
   bool sc_maxr_ok = true;
+  uint32_t sc_capsel_or = 0;  // OR of the per-scenario cap_sel overrides (0: none given)
+  int sc_pswitch_any = -1;    // any per-scenario peak_switch set (-1: none given)
   D1Params d1{};
   std::vector<uint32_t> zmasks;
   std::vector<double> h_cw;  // per-scenario carbon weights (empty: world default)
@@ -204,7 +206,8 @@ static int d1_check_world(ccka_ctx* c) {
   c->d1_ready = false;
   const ccka_deployment& dp = w.deploy[0];
   if (w.n_deploy != 1 || dp.scaler != CCKA_SCALER_HPA) return CCKA_OK;
-  if (w.disrupt_ext) return CCKA_OK;  // drift / replacement run on the general kernel
+  // drift / replacement run on the general kernel unless d1_prepare proves
+  // them inert for these scenarios (d1_disrupt_inert)
   for (int q = 0; q < w.n_pools; ++q)
     if (w.pools[q].limit_cpu_m >= 0) return CCKA_OK;
   if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
@@ -286,11 +289,59 @@ static int d1_check_world(ccka_ctx* c) {
   return CCKA_OK;
 }
 
+// The single-deployment kernel has no drift / replacement phases; it may run a
+// world that enables them only when they provably never act (exact):
+//  - drift needs a profile change that moves a pool's zone or capacity-type
+//    mask: never when no scenario switches, or OFFPEAK and PEAK resolve to the
+//    same masks for every pool;
+//  - replacement needs an on-demand node in a WhenEmptyOrUnderutilized pool:
+//    never when no pool profile uses that policy or no scenario's nodeSelector
+//    admits on-demand.
+static bool d1_disrupt_inert(const ccka_ctx* c) {
+  const ccka_world& w = c->hw;
+  if (w.disrupt_ext & CCKA_DISRUPT_DRIFT) {
+    const bool switching = c->sc_pswitch_any >= 0 ? c->sc_pswitch_any != 0 : w.peak_switch != 0;
+    bool same = true;
+    for (int q = 0; q < w.n_pools; ++q) {
+      uint32_t zm = 0, cm = 0;
+      for (const ccka_pool_patch* x : {&w.pools[q].base, &w.pools[q].profile[CCKA_PROFILE_RESET]}) {
+        if (x->zone_mask) zm = x->zone_mask;
+        if (x->cap_mask) cm = x->cap_mask;
+      }
+      // masks after the first profile (t = 0, either one) must never change
+      // over the alternations that follow (merge: 0 keeps the previous mask)
+      const ccka_pool_patch* pr[2] = {&w.pools[q].profile[CCKA_PROFILE_OFFPEAK],
+                                      &w.pools[q].profile[CCKA_PROFILE_PEAK]};
+      for (int first = 0; first < 2; ++first) {
+        uint32_t z = zm, k = cm, z1 = 0, k1 = 0;
+        for (int j = 0; j < 4; ++j) {
+          const ccka_pool_patch* x = pr[(first + j) & 1];
+          if (x->zone_mask) z = x->zone_mask;
+          if (x->cap_mask) k = x->cap_mask;
+          if (j == 0) { z1 = z; k1 = k; }
+          else if (z != z1 || k != k1) same = false;
+        }
+      }
+    }
+    if (switching && !same) return false;
+  }
+  if (w.disrupt_ext & CCKA_DISRUPT_REPLACE) {
+    bool weou = false;
+    for (int q = 0; q < w.n_pools; ++q) {
+      weou |= w.pools[q].base.policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
+      for (int s = 0; s < 3; ++s) weou |= w.pools[q].profile[s].policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
+    }
+    const uint32_t sel = c->sc_capsel_or ? c->sc_capsel_or : w.deploy[0].cap_sel;
+    if (weou && (sel & CCKA_CAP_OD)) return false;
+  }
+  return true;
+}
+
 // scenario-dependent part: distinct carbon weights, per-scenario index, tables
 static int d1_prepare(ccka_ctx* c) {
   c->d1_ready = true;
   c->d1_ok = false;
-  if (!c->d1_world || !c->sc_maxr_ok) return CCKA_OK;
+  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_inert(c)) return CCKA_OK;
   const size_t n = (size_t)c->N;
   std::vector<double> wl;
   std::vector<uint8_t> wci;
@@ -551,6 +602,14 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->h_cw.clear();
   if (sc->carbon_weight) c->h_cw.assign(sc->carbon_weight, sc->carbon_weight + n);
+  c->sc_capsel_or = 0;
+  if (sc->cap_sel)
+    for (size_t i = 0; i < n; ++i) c->sc_capsel_or |= sc->cap_sel[i];
+  c->sc_pswitch_any = -1;
+  if (sc->peak_switch) {
+    c->sc_pswitch_any = 0;
+    for (size_t i = 0; i < n; ++i) c->sc_pswitch_any |= sc->peak_switch[i] != 0;
+  }
   c->sc_maxr_ok = true;
   if (sc->max_replicas)
     for (size_t i = 0; i < n; ++i)

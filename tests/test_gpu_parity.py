@@ -421,3 +421,28 @@ def test_replacement_parity_multi_deployment(engine):
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
     assert ((tc["flags"] & 32) != 0).any()
     compare(rg, rc, tg, tc)
+
+
+def test_inert_disruption_runs_on_d1(engine):
+    """Worlds that enable drift / replacement where neither can ever act run on
+    the single-deployment kernel and still match the oracle (which runs the
+    phases); a world where they can act runs on the general kernel."""
+    spec = configs.config2_world(n_steps=720)
+    spec.replace = 1
+    sc = configs.hpa_scenarios(1200)
+    run_engine(engine, spec, sc, load=po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n))
+    assert engine.last_engine()[0] == 1  # half the scenarios select on-demand: not inert
+    sc.cap_sel = np.full(sc.n, abi.CAP_SPOT, np.uint8)  # spot-only: no on-demand node can exist
+    load = po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
+    spec.drift = 1  # zones move at the switch: drift can act
+    run_engine(engine, spec, sc, load=load)
+    assert engine.last_engine()[0] == 1
+    sc.peak_switch = np.zeros(sc.n, np.uint8)  # ... unless no scenario switches
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
