@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--drift", action="store_true",
                     help="configs 2-4 with Karpenter drift at the zone switch (SEMANTICS 3.G0; general kernel)")
+    ap.add_argument("--replace", action="store_true",
+                    help="configs 2-4 with single-node replacement consolidation (SEMANTICS 3.G2)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +118,7 @@ def main():
             gen = configs.config4_trace_gen()
             traj = (args.mode or "summary") == "trajectory"
         spec.drift = int(args.drift)
+        spec.replace = int(args.replace)
         eng.set_world(spec)
         eng.set_scenarios(sc)
         eng.gen_load(gen)
@@ -208,13 +211,14 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True,
             "scaling": "strong" if cfg == 3 else "weak", "vs_baseline": None, "dtype": "int32+int64+f64",
             "data": "synthetic (on-device Philox load traces, seed 20251205)",
-            "config": {"workload": workloads[cfg] + (" + Karpenter drift at the zone switch" if args.drift else ""),
+            "config": {"workload": workloads[cfg] + (" + Karpenter drift at the zone switch" if args.drift else "")
+                       + (" + replacement consolidation" if args.replace else ""),
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
                        "parallelism": f"scenario-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None if args.drift else measured_traffic(cfg, traj, N, T),
+                         "traffic": None if args.drift or args.replace else measured_traffic(cfg, traj, N, T),
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},
