@@ -933,6 +933,54 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           rdy &= ~(1u << b);
           unlink(b);
         };
+        // cheapest single offering (price, k, z, c) that holds the sums under a
+        // pool's zone / capacity-type masks and CPU limit
+        auto find_offer = [&](uint32_t zm, uint32_t cm, int use, int limit, int s_cpu, int s_mem, int s_pods,
+                              int& bk, int& bz, int& bc, int& bpr) {
+          bk = -1; bz = 0; bc = 0; bpr = 0;
+          for (int k = 0; k < L.K; ++k) {
+            if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
+            if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+            for (int z = 0; z < L.Z; ++z) {
+              if (!(zm >> z & 1u)) continue;
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                if (!(cm & capbit(c))) continue;
+                const int pr = tprice(L, rl, k, z, c);
+                if (pr > 0 && (bk < 0 || pr < bpr)) { bk = k; bz = z; bc = c; bpr = pr; }
+              }
+            }
+          }
+        };
+        // a pre-spun replacement node for slot `src` (no pods until it takes over)
+        auto launch_replacement = [&](int q, int slot, int src, int bk, int bz, int bc, int bpr) {
+          const bool now_ready = delay == 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (n == slot) {
+              ninfo[n] = ni_make(q, bk, bz, bc);
+              nready[n] = t + delay;
+              nlast[n] = t;
+              nprice[n] = bpr;
+              ncap[n] = DMAX == 1 ? L.cap1[bk] : 0;
+              nsrc[n] = src + 1;
+#pragma unroll
+              for (int e = 0; e < DMAX; ++e) npods[n][e] = 0;
+            }
+          }
+          used |= 1u << slot;
+          if (now_ready) rdy |= 1u << slot;
+          else next_ready = min(next_ready, t + delay);
+#pragma unroll
+          for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq) if (qq == q) puse[qq] += L.types[bk].vcpu * 1000;
+          if (bc == 0) nsp++; else nod++;
+          burn += bpr;
+          launches++;
+          last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+          hash = (hash ^ last_choice) * 16777619u;
+          step_last_type = bk;
+          flags |= 2u | 32u;
+        };
         // ---- G2. single-node replacement consolidation (SEMANTICS 3.G2): the
         // first candidate in (pods asc, price desc, slot asc) order that is
         // on-demand, has pods, is not being replaced and has a strictly cheaper
@@ -983,53 +1031,16 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             }
             cand &= ~(1u << best);
             if (pdb_pods > allowed || !cm) continue;
-            int bk = -1, bz = 0, bc = 0, bpr = 0;
-            for (int k = 0; k < L.K; ++k) {
-              if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
-              if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
-              for (int z = 0; z < L.Z; ++z) {
-                if (!(zm >> z & 1u)) continue;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                  if (!(cm & capbit(c))) continue;
-                  const int pr = tprice(L, rl, k, z, c);
-                  if (pr > 0 && (bk < 0 || pr < bpr)) { bk = k; bz = z; bc = c; bpr = pr; }
-                }
-              }
-            }
+            int bk, bz, bc, bpr;
+            find_offer(zm, cm, use, limit, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
             if (bk < 0 || bpr >= bprice) continue;
-            const bool now_ready = delay == 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              if (n == slot) {
-                ninfo[n] = ni_make(q, bk, bz, bc);
-                nready[n] = t + delay;
-                nlast[n] = t;
-                nprice[n] = bpr;
-                ncap[n] = DMAX == 1 ? L.cap1[bk] : 0;
-                nsrc[n] = best + 1;
-#pragma unroll
-                for (int e = 0; e < DMAX; ++e) npods[n][e] = 0;
-              }
-            }
-            used |= 1u << slot;
-            if (now_ready) rdy |= 1u << slot;
-            else next_ready = min(next_ready, t + delay);
-#pragma unroll
-            for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq) if (qq == q) puse[qq] += L.types[bk].vcpu * 1000;
-            if (bc == 0) nsp++; else nod++;
-            burn += bpr;
-            launches++;
-            last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
-            hash = (hash ^ last_choice) * 16777619u;
-            step_last_type = bk;
-            flags |= 2u | 32u;
+            launch_replacement(q, slot, best, bk, bz, bc, bpr);
             deleted++;
             break;
           }
         };
-        // ---- G1. ready replacements take over their source's pods (SEMANTICS 3.G2) ----
-        if (greplace) {
+        // ---- G1. ready replacements take over their source's pods (SEMANTICS 3.G0, 3.G2) ----
+        if (greplace || gdrift) {
           uint32_t rm = 0;
 #pragma unroll
           for (int m = 0; m < MAXN; ++m) rm |= ((nsrc[m] != 0) && (rdy >> m & 1u) ? 1u : 0u) << m;
@@ -1086,6 +1097,17 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             flags |= 4u;
           }
         }
+        // the PDB allowance counts after the takeovers (evictions change it)
+        if (pdb_pct >= 0) {
+          long long rdyp = 0, reps = 0;
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d) {
+            if (d >= D || !dep[d].pdb) continue;
+            reps += replicas[d];
+            rdyp += rpods[d];
+          }
+          allowed = max(rdyp - ((long long)pdb_pct * reps + 99) / 100, 0LL);
+        }
         // drifted nodes (SEMANTICS 3.G0): zone / capacity type outside the
         // pool's current requirements
         uint32_t dmask = 0;
@@ -1115,7 +1137,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             uint32_t pq = 0;
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) pq |= (ni_pool(ninfo[n]) == q ? 1u : 0u) << n;
-            uint32_t cand = dmask & rdy & pq;
+            uint32_t srcm = 0;  // nodes whose pre-spun replacement is in flight wait for it
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) if (nsrc[n]) srcm |= 1u << (nsrc[n] - 1);
+            uint32_t cand = dmask & rdy & pq & ~srcm;
             while (cand && deleted < budget) {
               const int best = __builtin_ctz(cand);
               cand &= cand - 1u;
@@ -1132,9 +1157,11 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               // pods move first-fit onto ready, non-drifted nodes; the rest are
               // evicted (Pending until E/F of a later step)
               const uint32_t recv = rdy & ~dmask;
+              int left[DMAX];
 #pragma unroll
               for (int d = 0; d < DMAX; ++d) {
-                if (d >= D) break;
+                left[d] = 0;
+                if (d >= D) continue;
                 int need_d = bp[d];
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n) {
@@ -1158,27 +1185,47 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                     if (k > 0) { npods[n][d] += k; need_d -= k; nlast[n] = t; }
                   }
                 }
-                rpods[d] -= need_d;
-                placed[d] -= need_d;
+                left[d] = need_d;
               }
-              int bprice = 0;
+              // pods that found no room: a pre-spun replacement under the new
+              // requirements takes them when ready (G1); without a free slot
+              // or an offering they are evicted and the node goes now
+              int s_cpu = 0, s_mem = 0, s_pods = 0;
+              uint32_t cm = 0, zm = 0;
+              int use = 0, limit = 0;
 #pragma unroll
-              for (int n = 0; n < MAXN; ++n) {
-                if (n == best) {
-                  bprice = nprice[n];
-                  if (ni_cap(ninfo[n]) == 0) nsp--; else nod--;
+              for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+                if (qq == q) { cm = pcm[qq]; zm = pzm[qq]; use = puse[qq]; limit = plimit[qq]; }
 #pragma unroll
-                  for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
-                    if (qq == q) puse[qq] -= L.types[ni_type(ninfo[n])].vcpu * 1000;
-                  ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
-#pragma unroll
-                  for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
-                }
+              for (int d = 0; d < DMAX; ++d) {
+                if (d >= D || left[d] <= 0) continue;
+                cm &= capsel[d];
+                s_cpu += left[d] * dep[d].req_cpu;
+                s_mem += left[d] * dep[d].req_mem;
+                s_pods += left[d];
               }
-              burn -= bprice;
-              used &= ~(1u << best);
-              unlink(best);
-              rdy &= ~(1u << best);
+              const uint32_t fr = ~used & slot_mask;
+              int bk = -1, bz = 0, bc = 0, bpr = 0;
+              if (s_pods > 0 && fr && cm) find_offer(zm, cm, use, limit, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
+              if (bk >= 0) {
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n)
+                  if (n == best) {
+#pragma unroll
+                    for (int d = 0; d < DMAX; ++d) npods[n][d] = d < D ? left[d] : 0;
+                  }
+                launch_replacement(q, __builtin_ctz(fr), best, bk, bz, bc, bpr);
+                allowed -= pdb_pods;
+                deleted++;
+                flags |= 16u;
+                continue;
+              }
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                rpods[d] -= left[d];
+                placed[d] -= left[d];
+              }
+              free_slot(best);
               dmask &= ~(1u << best);
               allowed -= pdb_pods;
               deleted++;

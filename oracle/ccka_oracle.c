@@ -334,6 +334,44 @@ static void o_free(o_node* nodes, int NN, int n) {
     if (nodes[m].src1 == n + 1) nodes[m].src1 = 0;
 }
 
+/* cheapest single offering (price, k, z, c) holding the sums under zone mask
+ * zm, capacity mask cm and the pool CPU limit; -1 if none (SEMANTICS 3.G2) */
+static int o_offer(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, int64_t use, int32_t limit,
+                   int64_t sc, int64_t sm, int64_t sp, int* bz, int* bc, int32_t* bp) {
+  int bk = -1;
+  for (int k = 0; k < e->K; ++k) {
+    const ccka_itype* ty = &e->w->types[k];
+    if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, sc, sm, sp, 0, 0) < 0) continue;
+    if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+    for (int z = 0; z < e->Z; ++z) {
+      if (!(zm >> z & 1u)) continue;
+      for (int cc = 0; cc < 2; ++cc) {
+        if (!(cm & (uint32_t)o_capidx_bit(cc))) continue;
+        const int32_t pr = o_price(e, r, h, k, z, cc);
+        if (pr > 0 && (bk < 0 || pr < *bp)) { bk = k; *bz = z; *bc = cc; *bp = pr; }
+      }
+    }
+  }
+  return bk;
+}
+
+/* a pre-spun replacement for slot src, no pods until it takes over */
+static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, int ready, int t, int src) {
+  o_node* nd = &st->nodes[slot];
+  memset(nd, 0, sizeof *nd);
+  nd->used = 1;
+  nd->pool = p;
+  nd->type = bk;
+  nd->zone = bz;
+  nd->cap = bc;
+  nd->ready_step = ready;
+  nd->last_event = t;
+  nd->src1 = src + 1;
+  st->launches++;
+  st->last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)p << 16;
+  st->hash = (st->hash ^ st->last_choice) * 16777619u;
+}
+
 static int o_drifted(const o_state* st, const o_node* nd) {
   const o_pool* pl = &st->pools[nd->pool];
   return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
@@ -646,7 +684,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       /* G1. replacements that are ready take over their source node's pods
        * (docs/SEMANTICS.md 3.G2), slot order; pods that no longer fit are
        * evicted; the source is deleted */
-      for (int m = 0; (w->disrupt_ext & CCKA_DISRUPT_REPLACE) && m < NN; ++m) {
+      for (int m = 0; (w->disrupt_ext & (CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE)) && m < NN; ++m) {
         o_node* rn = &st.nodes[m];
         if (!rn->used || !rn->src1 || rn->ready_step > t) continue;
         const int n = rn->src1 - 1;
@@ -688,11 +726,15 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
         for (int n = 0; (w->disrupt_ext & CCKA_DISRUPT_DRIFT) && n < NN && deleted < budget; ++n) {
           o_node* dn = &st.nodes[n];
           if (!dn->used || dn->pool != p || dn->ready_step > t || !o_drifted(&st, dn)) continue;
+          int src = 0;  /* its pre-spun replacement is in flight: wait for it */
+          for (int m = 0; m < NN; ++m) src |= st.nodes[m].src1 == n + 1;
+          if (src) continue;
           int64_t pdb_pods = 0;
           for (int d = 0; d < D; ++d) if (w->deploy[d].pdb_member) pdb_pods += dn->pods[d];
           if (pdb_pods > allowed) continue;
           /* pods move first-fit onto ready, non-drifted nodes; the rest are
            * evicted and Pending until F places or provisions them */
+          int left[CCKA_MAX_DEPLOY];
           for (int d = 0; d < D; ++d) {
             int need = dn->pods[d];
             for (int m = 0; m < NN && need > 0; ++m) {
@@ -702,6 +744,38 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
               const int64_t f = o_node_fit(e, nd, d);
               const int k = (int)(f < need ? f : need);
               if (k > 0) { nd->pods[d] += k; need -= k; nd->last_event = t; }
+            }
+            left[d] = need;
+          }
+          /* pods that found no room: a pre-spun replacement under the new
+           * requirements takes them when ready (G1); without a free slot or
+           * an offering they are evicted and the node goes now */
+          {
+            int64_t sc = 0, sm = 0, sp = 0, use = 0;
+            uint32_t cm = st.pools[p].cap_mask;
+            for (int d = 0; d < D; ++d) {
+              if (left[d] <= 0) continue;
+              cm &= capsel[d];
+              sc += (int64_t)left[d] * w->deploy[d].req_cpu_m;
+              sm += (int64_t)left[d] * w->deploy[d].req_mem_mi;
+              sp += left[d];
+            }
+            int slot = -1;
+            for (int m = 0; m < NN; ++m) if (!st.nodes[m].used) { slot = m; break; }
+            for (int m = 0; m < NN; ++m)
+              if (st.nodes[m].used && st.nodes[m].pool == p) use += (int64_t)w->types[st.nodes[m].type].vcpu * 1000;
+            int bz = 0, bc = 0, bk = -1;
+            int32_t bp = 0;
+            if (sp > 0 && slot >= 0 && cm)
+              bk = o_offer(e, r, h, st.pools[p].zone_mask, cm, use, w->pools[p].limit_cpu_m, sc, sm, sp, &bz, &bc, &bp);
+            if (bk >= 0) {
+              for (int d = 0; d < D; ++d) dn->pods[d] = left[d];
+              o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, n);
+              step_last_type = (uint16_t)bk;
+              allowed -= pdb_pods;
+              deleted++;
+              flags |= 2 | 16 | 32;
+              continue;
             }
           }
           o_free(st.nodes, NN, n);
@@ -797,35 +871,11 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           for (int n = 0; n < NN; ++n)
             if (st.nodes[n].used && st.nodes[n].pool == p) use += (int64_t)w->types[st.nodes[n].type].vcpu * 1000;
           const int32_t limit = w->pools[p].limit_cpu_m;
-          int bk = -1, bz = 0, bc = 0;
+          int bz = 0, bc = 0;
           int32_t bp = 0;
-          for (int k = 0; k < K; ++k) {
-            const ccka_itype* ty = &w->types[k];
-            if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
-            if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
-            for (int z = 0; z < e->Z; ++z) {
-              if (!(st.pools[p].zone_mask >> z & 1u)) continue;
-              for (int cc = 0; cc < 2; ++cc) {
-                if (!(cm & (uint32_t)o_capidx_bit(cc))) continue;
-                const int32_t pr = o_price(e, r, h, k, z, cc);
-                if (pr > 0 && (bk < 0 || pr < bp)) { bk = k; bz = z; bc = cc; bp = pr; }
-              }
-            }
-          }
+          const int bk = o_offer(e, r, h, st.pools[p].zone_mask, cm, use, limit, s_cpu, s_mem, s_pods, &bz, &bc, &bp);
           if (bk < 0 || bp >= bprice) { rej2[best] = 1; continue; }
-          o_node* nd = &st.nodes[slot];
-          memset(nd, 0, sizeof *nd);
-          nd->used = 1;
-          nd->pool = p;
-          nd->type = bk;
-          nd->zone = bz;
-          nd->cap = bc;
-          nd->ready_step = t + w->provision_delay_steps;
-          nd->last_event = t;
-          nd->src1 = best + 1;
-          st.launches++;
-          st.last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)p << 16;
-          st.hash = (st.hash ^ st.last_choice) * 16777619u;
+          o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, best);
           step_last_type = (uint16_t)bk;
           flags |= 2 | 32;
           deleted++;

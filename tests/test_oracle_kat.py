@@ -294,12 +294,15 @@ def test_pareto_known_answer():
 
 
 # ---------------------------------------------------------------- drift (SEMANTICS §3.G0)
-def test_drift_evicts_and_reprovisions_in_peak_zone():
+def test_drift_prespun_replacement_in_peak_zone():
     """5 static spot pods launch in us-east-2a (off-peak) at t=0. At t=10 the
     clock reaches 16:00 and PEAK narrows the zones to us-east-2c: with drift on
-    the node is deleted (no consolidateAfter wait), its pods are Pending at
-    t=10, re-provisioned at t=11 in zone c and running at t=12. Without drift
-    the node stays in zone a."""
+    the pods have no other node, so a replacement launches in zone c at t=10
+    (no consolidateAfter wait), takes the pods when ready at t=11 and the
+    drifted node is deleted; no pod is ever Pending after t=0. With a single
+    node slot there is no room for the replacement: the pods are evicted at
+    t=10, re-provisioned at t=11 and running at t=12. Without drift the node
+    stays in zone a."""
     d = deployment(abi.SCALER_STATIC, replicas0=5, min_r=5, max_r=5)
     spec = tiny_world([d], T=40, start_minute=950, pdb_pct=-1, drift=1)
     load = np.zeros((40, 1, 1), np.int32)
@@ -307,9 +310,17 @@ def test_drift_evicts_and_reprovisions_in_peak_zone():
     assert r["launches"][0] == 2 and r["deletions"][0] == 1
     assert (r["last_choice"][0] >> 12) & 3 == 2              # us-east-2c
     flags = tr["flags"][:, 0]
-    assert (flags[10] & 16) and (flags[10] & 4) and not (flags[:10] & 16).any()
-    assert list(tr["pending"][9:13, 0]) == [0, 5, 5, 0]
-    spec.drift = 0
+    assert (flags[10] & 16) and (flags[10] & 32) and (flags[10] & 2) and not (flags[10] & 4)
+    assert (flags[11] & 4) and not (flags[:10] & 16).any()
+    n = tr["nodes_spot"][:, 0]
+    assert n[9] == 1 and n[10] == 2 and n[11] == 1
+    assert (tr["pending"][1:, 0] == 0).all()
+    spec.max_nodes = 1
+    r1, tr1 = run(spec, load)
+    assert r1["launches"][0] == 2 and r1["deletions"][0] == 1
+    assert (tr1["flags"][10, 0] & 16) and (tr1["flags"][10, 0] & 4)
+    assert list(tr1["pending"][9:13, 0]) == [0, 5, 5, 0]
+    spec.max_nodes, spec.drift = 8, 0
     r0, tr0 = run(spec, load)
     assert r0["launches"][0] == 1 and r0["deletions"][0] == 0
     assert (r0["last_choice"][0] >> 12) & 3 == 0 and (tr0["pending"][1:, 0] == 0).all()
