@@ -54,11 +54,21 @@ def main():
                     help="configs 2-4 with Karpenter drift at the zone switch (SEMANTICS 3.G0; general kernel)")
     ap.add_argument("--replace", action="store_true",
                     help="configs 2-4 with single-node replacement consolidation (SEMANTICS 3.G2)")
+    ap.add_argument("--spawn", action="store_true",
+                    help="run the ranks as fresh child processes even at --gpus 1 (the launcher path)")
     args = ap.parse_args()
 
+    # one process per GPU: without a launcher's rank environment, this process
+    # only starts the N rank processes (it never touches a GPU itself)
+    from ccka import launch
+
+    if not launch.is_rank_process() and (args.gpus > 1 or args.spawn):
+        sys.exit(launch.spawn_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     import torch
 
     dist = None
@@ -67,15 +77,26 @@ def main():
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from ccka import configs
+    from ccka import abi, configs
     from ccka import dist as cdist
     from ccka.engine import Engine
 
     eng = Engine(local)
 
+    rccl = {}
+
     def comm_init():
-        uid = (C.c_uint8 * 128).from_buffer_copy(cdist.unique_id_exchange(eng, rank))
+        """RCCL communicator of libccka (also at one rank: the same exchange
+        code runs); records the rank count the communicator reports."""
+        if world > 1:
+            uid = (C.c_uint8 * 128).from_buffer_copy(cdist.unique_id_exchange(eng, rank))
+        else:
+            uid = (C.c_uint8 * 128)()
+            eng._chk(eng.lib.ccka_comm_unique_id(uid), "ccka_comm_unique_id")
         eng._chk(eng.lib.ccka_comm_init(eng.ctx, uid, world, rank), "ccka_comm_init")
+        nr, rk = C.c_int32(), C.c_int32()
+        eng._chk(eng.lib.ccka_comm_info(eng.ctx, C.byref(nr), C.byref(rk)), "ccka_comm_info")
+        rccl.update(nranks=nr.value, rank=rk.value)
 
     def barrier():
         if dist is not None:
@@ -122,7 +143,7 @@ def main():
         eng.set_world(spec)
         eng.set_scenarios(sc)
         eng.gen_load(gen)
-        if cfg == 4 and dist is not None:
+        if cfg == 4:
             comm_init()
         frontier = []
 
@@ -182,12 +203,12 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline_mlp(args.cpu_seconds)
     else:
-        totals = eng.totals()
-        if dist is not None and cfg != 4:
+        local_totals = eng.totals()
+        totals = abi.Totals.from_buffer_copy(local_totals)
+        if cfg != 4:
             comm_init()
-        if dist is not None:
-            # the cross-GPU exchange of the totals: RCCL all-reduce inside libccka
-            eng._chk(eng.lib.ccka_allreduce_totals(eng.ctx, C.byref(totals)), "ccka_allreduce_totals")
+        # the cross-GPU exchange of the totals: RCCL all-reduce inside libccka
+        eng._chk(eng.lib.ccka_allreduce_totals(eng.ctx, C.byref(totals)), "ccka_allreduce_totals")
         steps_total = (N * world if cfg != 3 else N * world) * T * K
         value = steps_total / elapsed
         # algorithmic bytes per launch: load [T][N] int32 read once (config 4:
@@ -215,7 +236,7 @@ def main():
                        + (" + replacement consolidation" if args.replace else ""),
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
-                       "parallelism": f"scenario-sharded x{world}"},
+                       "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None if args.drift or args.replace else measured_traffic(cfg, traj, N, T),
@@ -237,7 +258,8 @@ def main():
             out["roofline"]["copy_gbs"] = cbw
             out["roofline"]["frac_of_copy"] = achieved / cbw
         if rank == 0 and world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(eng, spec, sc, args.cpu_seconds)
+            out["cpu_baseline"], out["parity"], out["parity_detail"] = cpu_baseline(
+                eng, spec, sc, args.cpu_seconds, traj, local_totals)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
@@ -298,27 +320,105 @@ def profiled_issue(cfg):
     return d
 
 
-def cpu_baseline(eng, spec, sc, target_s):
-    """The CPU oracle (plain C restatement, gcc -O3, pthreads over contiguous
-    scenario shards) on the same workload: the same global ids and the same
-    device-generated traces (copied to the host, untimed). Whole batches up to
-    ~target_s of CPU time (a bounded prefix when one batch would take longer);
-    the median run is reported. A 1-thread figure on a prefix is added."""
+def host_cpu():
+    """Host CPU facts for the baseline: usable cores (affinity), nproc, the
+    cgroup CPU quota when one is set, and the /proc/cpuinfo model name."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": None,
+            "cgroup_cpus": None}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_cpus"] = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def oracle_native():
+    """Build the CPU oracle with -march=native for THIS host (the prebuilt one
+    is x86-64-v3 so that it loads on any box); returns (module, march)."""
+    import subprocess
+
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"], check=True, timeout=180,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        po.use_library(po.NATIVE_LIB)
+        return po, "native"
+    except Exception as e:  # the portable build still measures the same code
+        print(f"bench: -march=native oracle build failed ({e}); using the x86-64-v3 build", file=sys.stderr)
+        return po, "x86-64-v3"
+
+
+def cpu_baseline(eng, spec, sc, target_s, traj, gpu_totals):
+    """The CPU oracle (plain C restatement, gcc -O3 -march=native, pthreads
+    over contiguous scenario shards, one per usable host core) on the same
+    workload: the same global ids and the same device-generated traces (copied
+    to the host, untimed). Whole batches up to ~target_s of CPU time (a bounded
+    prefix when one batch would take longer); the median run is reported, plus
+    a 1-thread figure on a prefix.
+
+    Before timing, one untimed oracle run over the same batch (the whole
+    config-2 batch; a 1e5-scenario prefix of larger ones) is compared with the
+    GPU rollout field by field, with its trajectory when the rollout wrote one,
+    and with the device totals: the returned parity flag."""
+    po, march = oracle_native()
+    cpu = host_cpu()
+    # every core this process may run on: the affinity set, capped by the
+    # cgroup CPU quota when one is set (more threads than the quota only
+    # time-slice; the nproc-thread figure is reported beside it)
+    threads = max(1, cpu["affinity"])
+    if cpu["cgroup_cpus"]:
+        threads = max(1, min(threads, int(cpu["cgroup_cpus"])))
     load = eng.get_load()
     T = spec.n_steps
+    n = min(sc.n, 100_000)
 
-    def run(n, th):
-        sub = sc.slice(0, n)
-        ld = load if sc.n_traces else np.ascontiguousarray(load[:, :, :n])
+    def inputs(m):
+        sub = sc.slice(0, m)
+        ld = load if sc.n_traces else np.ascontiguousarray(load[:, :, :m])
+        return sub, ld
+
+    # ---- parity at the benchmark size (untimed) ----
+    sub, ld = inputs(n)
+    ref, ref_tr = po.rollout(spec, sub, ld, traj=traj, threads=threads)
+    got = eng.results()
+    bad = [k for k in ref if not np.array_equal(got[k][:n], ref[k])]
+    checked = ["results"]
+    if traj:
+        gtr = eng.trajectory()
+        if not np.array_equal(gtr[:, :n], ref_tr):
+            bad.append("trajectory")
+        checked.append("trajectory")
+        del gtr, ref_tr
+    if n == sc.n:
+        want = po.totals(ref, n)
+        for f, ct in abi_totals_fields():
+            a, b = getattr(gpu_totals, f), getattr(want, f)
+            # fp64 totals are sums in a different order (device tree vs serial)
+            if (a != b) if ct is not C.c_double else abs(a - b) > 1e-9 * abs(b):
+                bad.append(f"totals.{f}")
+        checked.append("totals")
+    parity = not bad
+    detail = {"scenarios": n, "of": sc.n, "steps": T, "checked": checked, "mismatched": bad,
+              "rule": "per-scenario results and trajectory bit-exact (integers, instance choices, fp64 "
+                      "energy/gCO2); totals: integers exact, fp64 sums <= 1e-9 relative"}
+
+    def run(m, th):
+        s2, l2 = inputs(m)
         t0 = time.perf_counter()
-        po.rollout(spec, sub, ld, threads=th)
+        po.rollout(spec, s2, l2, threads=th)
         return time.perf_counter() - t0
 
-    n = min(sc.n, 100_000)
     times = [run(n, threads)]
     while sum(times) < target_s and len(times) < 25:
         times.append(run(n, threads))
@@ -326,10 +426,23 @@ def cpu_baseline(eng, spec, sc, target_s):
     med = times[len(times) // 2]
     n1 = min(sc.n, 8192)
     t1 = run(n1, 1)
-    return {"value": n * T / med, "unit": "cluster-steps/s", "cores": threads, "kind": "port",
+    tn = None
+    if cpu["nproc"] and cpu["nproc"] != threads:
+        tn = min(run(n, cpu["nproc"]) for _ in range(3))
+    base = {"value": n * T / med, "unit": "cluster-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n} of {sc.n} scenarios x {T} steps, median of {len(times)} runs "
                       f"({med:.3f} s each) on {threads} threads",
-            "value_1thread": n1 * T / t1, "sample_1thread": f"{n1} scenarios x {T} steps, {t1:.2f} s"}
+            "value_1thread": n1 * T / t1, "sample_1thread": f"{n1} scenarios x {T} steps, {t1:.2f} s",
+            "nproc": cpu["nproc"], "cpu_model": cpu["cpu_model"], "cgroup_cpus": cpu["cgroup_cpus"],
+            "value_nproc_threads": None if tn is None else n * T / tn,
+            "build": f"gcc -O3 -march={march} -ffp-contract=off"}
+    return base, parity, detail
+
+
+def abi_totals_fields():
+    from ccka import abi
+
+    return abi.Totals._fields_
 
 
 def cpu_baseline_mlp(target_s):
@@ -339,7 +452,7 @@ def cpu_baseline_mlp(target_s):
 
     from ccka import configs
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = max(1, len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
     ws, bs = configs.mlp_weights(11)
     w = [torch.from_numpy(configs.from_bf16_bits(configs.to_bf16_bits(x))) for x in ws]

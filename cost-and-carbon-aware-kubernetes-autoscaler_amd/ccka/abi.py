@@ -185,6 +185,7 @@ def load_engine(path: str | None = None):
         "ccka_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "ccka_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
         "ccka_allreduce_totals": (C.c_int, [vp, C.POINTER(Totals)]),
+        "ccka_comm_info": (C.c_int, [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
         "ccka_device_info": (C.c_int, [vp, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
@@ -201,7 +202,7 @@ EXPORTED = [
     "ccka_set_world", "ccka_set_scenarios", "ccka_set_load", "ccka_gen_load", "ccka_get_load",
     "ccka_rollout", "ccka_rollout_async", "ccka_sync", "ccka_last_kernel_ms", "ccka_get_results",
     "ccka_get_trajectory", "ccka_get_totals", "ccka_comm_unique_id", "ccka_comm_init",
-    "ccka_allreduce_totals", "ccka_device_info", "ccka_get_grid_stats", "ccka_pareto_frontier",
+    "ccka_allreduce_totals", "ccka_comm_info", "ccka_device_info", "ccka_get_grid_stats", "ccka_pareto_frontier",
     "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
     "ccka_mlp_forward_async", "ccka_mlp_get_actions",
 ]

@@ -117,6 +117,44 @@ class Engine:
                   "ccka_pareto_frontier")
         return _grid_array(a, n.value)
 
+    # ---- multi-GPU (RCCL over xGMI) ----
+    def comm_init(self, uid: bytes | None = None, nranks: int = 1, rank: int = 0):
+        """RCCL communicator of this context; uid = None creates a fresh id
+        (one-rank communicator, or rank 0 before distributing it)."""
+        buf = (C.c_uint8 * 128)()
+        if uid is None:
+            self._chk(self.lib.ccka_comm_unique_id(buf), "ccka_comm_unique_id")
+        else:
+            buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._chk(self.lib.ccka_comm_init(self.ctx, buf, nranks, rank), "ccka_comm_init")
+
+    def comm_info(self):
+        n, r = C.c_int32(), C.c_int32()
+        self._chk(self.lib.ccka_comm_info(self.ctx, C.byref(n), C.byref(r)), "ccka_comm_info")
+        return n.value, r.value
+
+    def allreduce_totals(self, t: abi.Totals) -> abi.Totals:
+        out = abi.Totals.from_buffer_copy(t)
+        self._chk(self.lib.ccka_allreduce_totals(self.ctx, C.byref(out)), "ccka_allreduce_totals")
+        return out
+
+    def debug_pareto_merge(self, gathered: np.ndarray, counts, capacity: int | None = None) -> np.ndarray:
+        """Internal: the cross-rank merge of ccka_pareto_frontier on given
+        exchange buffers (gathered: GRID_DTYPE [nranks][cap])."""
+        g = np.ascontiguousarray(gathered, GRID_DTYPE)
+        nranks, cap = g.shape
+        cnt = np.ascontiguousarray(counts, np.int64)
+        assert cnt.shape == (nranks,)
+        outcap = capacity if capacity is not None else nranks * cap
+        a = (abi.GridStats * outcap)()
+        n = C.c_int32()
+        fn = self.lib.ccka_debug_pareto_merge
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p, C.c_int32,
+                       C.POINTER(C.c_int32)]
+        self._chk(fn(self.ctx, g.ctypes.data, cnt.ctypes.data, nranks, cap, a, outcap, C.byref(n)),
+                  "ccka_debug_pareto_merge")
+        return _grid_array(a, n.value)
+
     # ---- learned MLP policy (config 5) ----
     def mlp_set_weights(self, ws, bs):
         """ws: bf16 bit arrays (uint16) [in][out]; bs: float32 biases."""

@@ -99,7 +99,10 @@ struct ccka_ctx {
   int64_t* d_gcounts = nullptr;
   int32_t* d_gn = nullptr;
   uint8_t* d_gflags = nullptr;
+  ccka_grid_stats* d_gfront = nullptr;   // the frontier (local or global)
   int64_t gcap = 0;
+  int64_t pcap_ng = 0;
+  int pcap_ranks = 0;
   // learned MLP policy (config 5)
   bool mlp_have_w = false;
   mlp_bf16x8* d_w1f = nullptr;
@@ -449,7 +452,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
   dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_ggather); dfree(c->d_gcounts); dfree(c->d_gn);
-  dfree(c->d_gflags);
+  dfree(c->d_gflags); dfree(c->d_gfront);
   dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -952,6 +955,17 @@ int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
   return CCKA_OK;
 }
 
+int ccka_comm_info(ccka_ctx* c, int32_t* nranks, int32_t* rank) {
+  if (!c) return CCKA_EINVAL;
+  if (!c->comm) return fail(c, CCKA_ESTATE, "ccka_comm_init first");
+  int n = 0, r = 0;
+  if (ncclCommCount(c->comm, &n) != ncclSuccess || ncclCommUserRank(c->comm, &r) != ncclSuccess)
+    return fail(c, CCKA_ERCCL, "ncclCommCount / ncclCommUserRank failed");
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  return CCKA_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Policy sweep (BASELINE config 4)
 // ---------------------------------------------------------------------------
@@ -963,11 +977,8 @@ static int sweep_grids(ccka_ctx* c, int64_t grid_size, int64_t* n_grids) {
   const int64_t ng = c->N / grid_size;
   if (ng > (1 << 24)) return fail(c, CCKA_EINVAL, "too many grids");
   if (c->gcap < ng) {
-    dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_gflags); dfree(c->d_gn);
-    if (hipMalloc((void**)&c->d_gstats, sizeof(ccka_grid_stats) * ng) != hipSuccess ||
-        hipMalloc((void**)&c->d_gcand, sizeof(ccka_grid_stats) * ng) != hipSuccess ||
-        hipMalloc((void**)&c->d_gflags, (size_t)ng) != hipSuccess ||
-        hipMalloc((void**)&c->d_gn, 2 * sizeof(int32_t)) != hipSuccess)
+    dfree(c->d_gstats);
+    if (hipMalloc((void**)&c->d_gstats, sizeof(ccka_grid_stats) * ng) != hipSuccess)
       return fail(c, CCKA_ENOMEM, "grid buffers");
     c->gcap = ng;
   }
@@ -993,55 +1004,85 @@ int ccka_get_grid_stats(ccka_ctx* c, int64_t grid_size, ccka_grid_stats* out, in
   return CCKA_OK;
 }
 
+// Pareto buffers for `ng` local grids and `nranks` ranks: the local candidates
+// (ng), the all-gathered candidate rows [nranks][ng] followed by their union
+// (nranks * ng), the final frontier and the dominance flags (nranks * ng each:
+// the global frontier can hold every rank's candidates), the per-rank counts
+// (+ the local one) and two device-side sizes.
+static int pareto_bufs(ccka_ctx* c, int64_t ng, int nranks) {
+  const int64_t tot = ng * nranks;
+  if (c->pcap_ng < ng || c->pcap_ranks < nranks) {
+    dfree(c->d_gcand); dfree(c->d_gflags); dfree(c->d_gn); dfree(c->d_ggather); dfree(c->d_gcounts);
+    dfree(c->d_gfront);
+    if (hipMalloc((void**)&c->d_gcand, sizeof(ccka_grid_stats) * ng) != hipSuccess ||
+        hipMalloc((void**)&c->d_gfront, sizeof(ccka_grid_stats) * tot) != hipSuccess ||
+        hipMalloc((void**)&c->d_gflags, (size_t)tot) != hipSuccess ||
+        hipMalloc((void**)&c->d_gn, 2 * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc((void**)&c->d_ggather, sizeof(ccka_grid_stats) * tot * 2) != hipSuccess ||
+        hipMalloc((void**)&c->d_gcounts, sizeof(int64_t) * (nranks + 1)) != hipSuccess) {
+      c->pcap_ng = c->pcap_ranks = 0;
+      return fail(c, CCKA_ENOMEM, "pareto buffers (%lld grids x %d ranks)", (long long)ng, nranks);
+    }
+    c->pcap_ng = ng;
+    c->pcap_ranks = nranks;
+  }
+  return CCKA_OK;
+}
+
+// Global filter over the exchanged candidates, identical on every rank: the
+// valid prefixes of gathered[nranks][ng] (counts[q] each, rank order = grid
+// order) are compacted, then filtered again into d_gfront / d_gn[0].
+static int pareto_merge(ccka_ctx* c, int64_t ng, int nranks) {
+  ccka_grid_stats* uni = c->d_ggather + ng * nranks;
+  HIPCHK(c, launch_pareto_union(c->d_ggather, c->d_gcounts, nranks, (int)ng, uni, c->d_gn + 1, c->stream));
+  HIPCHK(c, launch_pareto(uni, (int)(ng * nranks), c->d_gn + 1, c->d_gflags, c->d_gfront, c->d_gn, c->stream));
+  return CCKA_OK;
+}
+
+static int pareto_copy_out(ccka_ctx* c, ccka_grid_stats* out, int32_t capacity, int32_t* n_out) {
+  int32_t n = 0;
+  HIPCHK(c, hipMemcpyAsync(&n, c->d_gn, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *n_out = n;
+  if (n > capacity) return fail(c, CCKA_EINVAL, "frontier has %d grids, capacity %d", n, capacity);
+  if (n > 0) {
+    HIPCHK(c, hipMemcpyAsync(out, c->d_gfront, sizeof(ccka_grid_stats) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return CCKA_OK;
+}
+
 int ccka_pareto_frontier(ccka_ctx* c, int64_t grid_size, ccka_grid_stats* out, int32_t capacity, int32_t* n_out) {
   if (!c || !n_out || capacity < 0 || (capacity > 0 && !out)) return CCKA_EINVAL;
   (void)hipSetDevice(c->device);
   int64_t ng = 0;
   int rc;
   if ((rc = sweep_grids(c, grid_size, &ng)) != CCKA_OK) return rc;
-  // local frontier: non-dominated grids of this rank, in grid order
+  int nranks = 1;
+  if (c->comm && ncclCommCount(c->comm, &nranks) != ncclSuccess)
+    return fail(c, CCKA_ERCCL, "ncclCommCount failed");
+  if ((rc = pareto_bufs(c, ng, nranks)) != CCKA_OK) return rc;
+  if (!c->comm) {
+    // local frontier only: non-dominated grids of this batch, in grid order
+    HIPCHK(c, launch_pareto(c->d_gstats, (int)ng, nullptr, c->d_gflags, c->d_gfront, c->d_gn, c->stream));
+    return pareto_copy_out(c, out, capacity, n_out);
+  }
+  // local candidates, then the exchange: every rank's candidates (fixed
+  // capacity = grids per rank, every rank holds the same number) and counts
   HIPCHK(c, launch_pareto(c->d_gstats, (int)ng, nullptr, c->d_gflags, c->d_gcand, c->d_gn, c->stream));
-  const ccka_grid_stats* front = c->d_gcand;
-  const int32_t* front_n = c->d_gn;
-  if (c->comm) {
-    // exchange: every rank's candidates (fixed capacity = grids per rank) and counts
-    int nranks = 1;
-    ncclCommCount(c->comm, &nranks);
-    dfree(c->d_ggather);
-    dfree(c->d_gcounts);
-    if (hipMalloc((void**)&c->d_ggather, sizeof(ccka_grid_stats) * ng * nranks * 2) != hipSuccess ||
-        hipMalloc((void**)&c->d_gcounts, sizeof(int64_t) * (nranks + 1)) != hipSuccess)
-      return fail(c, CCKA_ENOMEM, "pareto gather buffers");
-    int64_t* cnt_local = c->d_gcounts + nranks;
-    // int32 count -> int64 slot (device copy keeps the exchange on the stream)
-    HIPCHK(c, hipMemsetAsync(cnt_local, 0, sizeof(int64_t), c->stream));
-    HIPCHK(c, hipMemcpyAsync(cnt_local, c->d_gn, sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
-    ccka_grid_stats* gathered = c->d_ggather;
-    ccka_grid_stats* uni = c->d_ggather + ng * nranks;
-    uint8_t* gflags = reinterpret_cast<uint8_t*>(c->d_gstats);  // grid stats no longer needed
-    ncclGroupStart();
-    ncclResult_t r1 = ncclAllGather(cnt_local, c->d_gcounts, 1, ncclInt64, c->comm, c->stream);
-    ncclResult_t r2 = ncclAllGather(c->d_gcand, gathered, (size_t)ng * sizeof(ccka_grid_stats), ncclUint8,
-                                    c->comm, c->stream);
-    ncclResult_t r3 = ncclGroupEnd();
-    if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
-      return fail(c, CCKA_ERCCL, "ncclAllGather (pareto candidates) failed");
-    HIPCHK(c, launch_pareto_union(gathered, c->d_gcounts, nranks, (int)ng, uni, c->d_gn + 1, c->stream));
-    HIPCHK(c, launch_pareto(uni, (int)(ng * nranks), c->d_gn + 1, gflags, c->d_gcand, c->d_gn,
-                            c->stream));
-    front = c->d_gcand;
-    front_n = c->d_gn;
-  }
-  int32_t n = 0;
-  HIPCHK(c, hipMemcpyAsync(&n, front_n, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  *n_out = n;
-  if (n > capacity) return fail(c, CCKA_EINVAL, "frontier has %d grids, capacity %d", n, capacity);
-  if (n > 0) {
-    HIPCHK(c, hipMemcpyAsync(out, front, sizeof(ccka_grid_stats) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
-  return CCKA_OK;
+  int64_t* cnt_local = c->d_gcounts + nranks;
+  // int32 count -> int64 slot (device copy keeps the exchange on the stream)
+  HIPCHK(c, hipMemsetAsync(cnt_local, 0, sizeof(int64_t), c->stream));
+  HIPCHK(c, hipMemcpyAsync(cnt_local, c->d_gn, sizeof(int32_t), hipMemcpyDeviceToDevice, c->stream));
+  ncclGroupStart();
+  ncclResult_t r1 = ncclAllGather(cnt_local, c->d_gcounts, 1, ncclInt64, c->comm, c->stream);
+  ncclResult_t r2 = ncclAllGather(c->d_gcand, c->d_ggather, (size_t)ng * sizeof(ccka_grid_stats), ncclUint8,
+                                  c->comm, c->stream);
+  ncclResult_t r3 = ncclGroupEnd();
+  if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
+    return fail(c, CCKA_ERCCL, "ncclAllGather (pareto candidates) failed");
+  if ((rc = pareto_merge(c, ng, nranks)) != CCKA_OK) return rc;
+  return pareto_copy_out(c, out, capacity, n_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -1223,6 +1264,28 @@ int ccka_debug_stamps(ccka_ctx* c, unsigned long long* out8) {
   if (!c || !out8 || !c->d_stamps) return CCKA_EINVAL;
   HIPCHK(c, hipMemcpy(out8, c->d_stamps, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return CCKA_OK;
+}
+
+// Internal (not in include/ccka.h): the cross-rank half of
+// ccka_pareto_frontier on caller-supplied exchange buffers, i.e. what every
+// rank runs after the RCCL all-gather: `gathered` [nranks][cap] candidate rows
+// (rank q's first counts[q] valid, each sorted by grid id, ranks in grid
+// order), merged and filtered into the global frontier. Lets a single GPU
+// exercise the multi-rank merge path.
+int ccka_debug_pareto_merge(ccka_ctx* c, const ccka_grid_stats* gathered, const int64_t* counts, int32_t nranks,
+                            int64_t cap, ccka_grid_stats* out, int32_t capacity, int32_t* n_out) {
+  if (!c || !gathered || !counts || !n_out || nranks < 1 || cap < 1 || capacity < 0 || (capacity > 0 && !out))
+    return CCKA_EINVAL;
+  for (int q = 0; q < nranks; ++q)
+    if (counts[q] < 0 || counts[q] > cap) return fail(c, CCKA_EINVAL, "count of rank %d out of range", q);
+  (void)hipSetDevice(c->device);
+  int rc;
+  if ((rc = pareto_bufs(c, cap, nranks)) != CCKA_OK) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_ggather, gathered, sizeof(ccka_grid_stats) * cap * nranks, hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_gcounts, counts, sizeof(int64_t) * nranks, hipMemcpyHostToDevice, c->stream));
+  if ((rc = pareto_merge(c, cap, nranks)) != CCKA_OK) return rc;
+  return pareto_copy_out(c, out, capacity, n_out);
 }
 
 int ccka_device_info(ccka_ctx* c, char* name, int32_t name_len, int32_t* cu_count) {

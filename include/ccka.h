@@ -329,6 +329,9 @@ int ccka_comm_unique_id(uint8_t* id128);
 int ccka_comm_init(ccka_ctx* ctx, const uint8_t* id128, int32_t nranks, int32_t rank);
 /* In-place sum of the packed totals across ranks. */
 int ccka_allreduce_totals(ccka_ctx* ctx, ccka_totals* inout);
+/* Rank count and this context's rank as the RCCL communicator reports them
+ * (ncclCommCount / ncclCommUserRank); CCKA_ESTATE without ccka_comm_init. */
+int ccka_comm_info(ccka_ctx* ctx, int32_t* nranks, int32_t* rank);
 
 /* ---- introspection ---------------------------------------------------- */
 /* Name and compute-unit count of the context's device. */

@@ -15,6 +15,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libccka_oracle.so")
+# the same source built -march=native on the host that runs it (bench.py's
+# CPU baseline builds it there: `make -C oracle native`)
+NATIVE_LIB = os.path.join(HERE, "build", "native", "libccka_oracle.so")
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "cost-and-carbon-aware-kubernetes-autoscaler_amd"))
 
 from ccka import abi  # noqa: E402
@@ -25,6 +28,14 @@ _LIB = None
 
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def use_library(path):
+    """Load the oracle from `path` (e.g. NATIVE_LIB) instead of LIB."""
+    global _LIB, LIB
+    LIB = path
+    _LIB = None
+    lib()
 
 
 def lib():
