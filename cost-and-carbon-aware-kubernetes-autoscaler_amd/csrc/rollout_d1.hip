@@ -220,13 +220,24 @@ __device__ __forceinline__ void ring_push(uint32_t* r, int v) {
   r[1] = __builtin_amdgcn_alignbit(r[1], r[0], 16);
   r[0] = (r[0] << 16) | ((uint32_t)v & 0xFFFFu);
 }
-__device__ __forceinline__ int ring_s(const uint32_t* r, int k) { return (int)(int16_t)(r[k >> 1] >> ((k & 1) * 16)); }
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ short2v as_s2(uint32_t x) { return __builtin_bit_cast(short2v, x); }
-__device__ __forceinline__ uint32_t as_u(short2v x) { return __builtin_bit_cast(uint32_t, x); }
 // (m & a) | (~m & b): v_bfi_b32
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+// floor(a / b) for 0 <= a < 2^31, 1 <= b < 2^30, given rb = 1/(float)b
+// (v_rcp_f32): the f32 estimate is within one of the quotient while the
+// quotient is below 2^20, and one remainder test corrects it; larger
+// quotients take the exact integer division (a branch no real input takes).
+__device__ __forceinline__ int fdiv_floor(int a, int b, float rb) {
+  int q = (int)((float)a * rb);
+  if (__builtin_expect(q >= (1 << 20) || b >= (1 << 30), 0)) return a / b;
+  // remainder in [-b, 2b): exact in 32-bit two's complement
+  const int r = (int)((uint32_t)a - (uint32_t)q * (uint32_t)b);
+  q += (r >= b ? 1 : 0) - (r < 0 ? 1 : 0);
+  return q;
+}
 
 // convertDesiredReplicasWithBehaviorRate, one direction. The period sums of
 // scale-up / scale-down deltas are packed int16 dot products of the delta
@@ -262,7 +273,7 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 }  // namespace
 
 // STAMPS: diagnostic build only (never in a real run): per-phase s_memtime
-// cycle totals summed over waves into p.stamps[8].
+// cycle totals summed over waves into p.stamps[12].
 #define D1_STAMP(k)                                          \
   if constexpr (STAMPS) {                                    \
     __builtin_amdgcn_sched_barrier(0);                       \
@@ -271,6 +282,12 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
     st_acc[k] += now_ - st_last;                             \
     st_last = now_;                                          \
   }
+
+// Load samples are prefetched PF steps ahead (a register FIFO): a step now
+// takes well under an HBM miss, and every in-step vector-memory wait (the
+// argmin-table row of a launch, the hourly price tile) also waits for all
+// older loads still in flight.
+constexpr int D1_PF = 3;
 
 template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
@@ -304,6 +321,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   while ((double)ulo / (double)target < p.tol_lo) ++ulo;
   int uhi = (int)floor(p.tol_hi * (double)target) + 2;
   while ((double)uhi / (double)target > p.tol_hi) --uhi;
+  const float rtarget = __builtin_amdgcn_rcpf((float)target);
 
   // ---- kernel arguments used inside the step loop (opaque register copies) ----
   const int NP = opq(p.NP), NZI = opq(p.NZI), NW = opq(p.NW), JT = opq(p.JT);
@@ -345,11 +363,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   }
 
   // consolidateAfter (steps) of a slot's pool: explicit selects on the pool
-  // bits (an indexed pcas[] would be demoted to scratch memory). Each slot
-  // carries its pool's value in sinfo bits 16..31 (clamped to 0xFFFF: with
-  // T <= 65535 a larger value never makes a node consolidatable either), so
-  // the per-touch update is one shift; this select runs only when a pool's
-  // value changes (profile switch) or a slot is created.
+  // bits (an indexed pcas[] would be demoted to scratch memory), clamped to
+  // 0xFFFF (with T <= 65535 a larger value never makes a node consolidatable
+  // either). Each slot keeps its pool's value in scas[] and its
+  // consolidatable-from step slc = last pod event + scas; it is a
+  // consolidation candidate iff it is ready and slc <= t.
   auto cas_of = [&](uint32_t info) {
     const int m1 = -(int)(info >> 13 & 1u), m2 = -(int)(info >> 14 & 1u);
     const int lo = pcas[0] ^ ((pcas[0] ^ pcas[MAXP > 1 ? 1 : 0]) & m1);
@@ -360,19 +378,21 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       return lo ^ ((lo ^ hi) & m2);
     }
   };
+  auto casc = [](int c) { return min(c, 0xFFFF); };
 
   // ---- node slots (register arrays, fully unrolled loops) ----
-  uint32_t sinfo[MAXN];  // type | zone<<10 | cap<<12 | pool<<13 | consolidateAfter steps<<16
-  auto cas16 = [](int c) { return (uint32_t)min(c, 0xFFFF) << 16; };
-  int sready[MAXN], slast[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN], selig[MAXN];
+  // Fields of a free slot are stale: every use is masked by `used` (or by
+  // `rdy` / the candidate masks, subsets of it), except sallocr, which is
+  // zero on every slot that is not ready (accounting reads it unmasked).
+  uint32_t sinfo[MAXN];  // type | zone<<10 | cap<<12 | pool<<13
+  int sready[MAXN], slc[MAXN], scas[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN];
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
-  float sinvf[MAXN];    // 1/alloc (saturation pre-test only; the energy itself is exact)
   int salloc[MAXN];     // alloc_cpu_m of the slot's type (< 2^24 by eligibility)
+  int sallocr[MAXN];    // salloc once the node is ready, else 0
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
-    sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0; selig[n] = 0;
-    sdyn[n] = 0; sinvf[n] = 0.f; salloc[n] = 0;
-
+    sinfo[n] = 0; sready[n] = 0; slc[n] = 0; scas[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
+    sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0;
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
   const uint32_t slot_mask = maxn >= 32 ? 0xFFFFFFFFu : ((1u << maxn) - 1u);
@@ -380,7 +400,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int replicas = p.replicas0, placed = 0, rpods = 0;
   // HPA history, packed int16, entry k = k+1 steps old at decision time:
   // recommendations with invalid entries stored as the neutral element of the
-  // max (hdn) and of the min (hup), and scale deltas
+  // max (hdn) and of the min (hup), and scale deltas. With the default
+  // behavior only the down window reads history (no up window, 15 s periods).
   uint32_t hdn[4], hup[4], hdel[4] = {0, 0, 0, 0};
   uint32_t dn16[4];  // this scenario's down-stabilisation window as packed lane masks
 #pragma unroll
@@ -390,23 +411,15 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     dn16[w] = ((dnmask >> (2 * w)) & 1 ? 0xFFFFu : 0u) | ((dnmask >> (2 * w + 1)) & 1 ? 0xFFFF0000u : 0u);
   }
   int next_ready = 0x7fffffff, nsp = 0, nod = 0;
-  // free pod capacity of the compatible ready slots (kept incrementally:
-  // readiness, reconcile of running pods, scheduling onto ready slots,
-  // zero-delay launches; recomputed after a deletion)
+  // free pod capacity of the compatible ready slots (kept incrementally)
   int Ffree = 0;
-  bool dirty = true;
-  int wake = 0;
+  // smallest pod capacity of any node launched so far (refreshed on deletion):
+  // an under-utilised node can only be deleted when F >= its capacity
+  int minscap = 0x7fffffff;
   int profile = -1, hour = -1;
   long long cost = 0, burn = 0, base_price = 0;
   int pend_min = 0;  // <= 32767 pods x T steps
-  // energy in exact nanowatt-minutes. Cached over the slots (refreshed when a
-  // slot's pods, readiness or existence changed): I = sum of idle draw,
-  // S = sum over ready slots of dyn_nw_per_m * pods, R = max over ready slots
-  // of pods/alloc in binary32: upp*R < 0.9999 proves no node saturates, and
-  // then the step's energy is base + I + upp*S exactly.
-  long long energy_nw = 0, e_hour = 0, Isum = 0, Ssum = 0;
-  float Rmax = 0.f;
-  bool acc_dirty = false;
+  long long energy_nw = 0, e_hour = 0, Isum = 0;  // exact nanowatt-minutes; Isum: idle draw of used slots
   double gco2 = 0.0, ci_min = 0.0;
   int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
   uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
@@ -419,23 +432,23 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
   };
 
-  // load samples software-pipelined one step ahead: a step is long enough to
-  // cover the HBM latency of the next step's coalesced read
   // load column: the scenario's own trace, or its shared trace (policy sweeps)
   const int32_t* lp = p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
   const long long lsl = opq(p.NL);
   // Memory pipeline of one step: at its top the previous step's trajectory
-  // record is stored and the next step's load sample is issued; the sample is
-  // taken into a register only at the end of the step, so every wait the
-  // compiler places covers operations that are a whole step old.
-  int Lcur = opqv(lp[0]);
+  // record is stored and the load sample D1_PF steps ahead is issued; a sample
+  // enters the FIFO only at the end of its issuing step (opqv), so every wait
+  // the compiler places covers operations at least a step old.
+  int Lq[D1_PF];
+#pragma unroll
+  for (int k = 0; k < D1_PF; ++k) Lq[k] = opqv(lp[(int64_t)min(k, T - 1) * lsl]);
   int4 rec_prev = make_int4(0, 0, 0, 0);
   int minute = p.start_minute % 1440;
 
   for (int t = 0; t < T; ++t, minute = minute == 1439 ? 0 : minute + 1) {
     if (traj && t > 0) *(int4*)(traj + (int64_t)(t - 1) * ls + i) = rec_prev;
-    const int Lraw = lp[(int64_t)min(t + 1, T - 1) * lsl];
-    const int L = Lcur;
+    const int Lraw = lp[(int64_t)min(t + D1_PF, T - 1) * lsl];
+    const int L = Lq[0];
     const int h = minute / 60;
     const int rh = r * 24 + h;
     if (h != hour) {  // wave-uniform: this hour's prices and carbon intensity
@@ -475,13 +488,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           if (sready[n] <= t) {
             rdy |= 1u << n;
             rpods += spods[n];
-            acc_dirty = true;
+            sallocr[n] = salloc[n];
             if (cmask >> n & 1u) Ffree += scap[n] - spods[n];
           }
           else next_ready = min(next_ready, sready[n]);
         }
       }
-      dirty = true;
     }
     // ---- A. profile ----
     const bool in_win = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
@@ -490,7 +502,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     if (peak) flags |= 1u;
     if (prof != profile) {
       profile = prof;
-      dirty = true;
 #pragma unroll
       for (int q = 0; q < MAXP; ++q) {
         if (q >= NP) break;
@@ -504,14 +515,22 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int n = 0; n < MAXN; ++n)
         if (used >> n & 1u) {
-          sinfo[n] = (sinfo[n] & 0xFFFFu) | cas16(cas_of(sinfo[n]));
-          selig[n] = max(sready[n], slast[n] + (int)(sinfo[n] >> 16));
+          const int c = casc(cas_of(sinfo[n]));
+          slc[n] += c - scas[n];
+          scas[n] = c;
         }
       refresh_J(rh);
     }
 
     D1_STAMP(1);
-    // ---- C. HPA ----
+    // ---- C. HPA (replica_calculator.go + horizontal.go, SEMANTICS §3.C) ----
+    // util = int32(usage*100 / (ready*req)) by an f32-reciprocal division with
+    // an exact remainder correction; the tolerance band, the unready rule and
+    // the SLO threshold are integer tests on util (exactly the binary64 tests
+    // of the spec, see ulo/uhi). The proposal ceil(fl(fl(util/target)*ready))
+    // equals the exact integer ceiling unless util*ready is a multiple of
+    // target (|rounding error| < 1/target otherwise); only that case runs the
+    // binary64 expression.
     const int cur = replicas, ready = rpods;
     int desired = cur, proposal = cur, util = 0;
     bool ran = false, hpa_path = true, util_valid = false;
@@ -524,25 +543,41 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     } else if (ready > 0) {
       const long long rcap = (long long)ready * limit;
       const int usage = (limit > 0 && rcap < (long long)L) ? (int)rcap : L;
-      // int32(usage*100 / (ready*req)): 32-bit unsigned division when it is exact
-      if (usage >= 0 && usage <= 42949672) util = (int)((uint32_t)usage * 100u / (uint32_t)(ready * req));
-      else util = (int)(((long long)usage * 100) / ((long long)ready * req));
+      const int dreq = ready * req;  // < 2^31: ready <= 32767, req <= 65535
+      if (__builtin_expect(usage >= 0 && usage <= 21474836, 1))
+        util = fdiv_floor(usage * 100, dreq, __builtin_amdgcn_rcpf((float)dreq));
+      else
+        util = (int)(((long long)usage * 100) / ((long long)dreq));
       util_valid = true;
       ran = true;
-      const bool unready_up = cur > ready && util > target;
-      if (unready_up || util < ulo || util > uhi) {  // scale event: binary64 as the spec writes it
-        const double ratio = (double)util / (double)target;
-        if (cur - ready > 0 && ratio > 1.0) {
-          const int nu = (usage >= 0 && usage <= 42949672)
-                             ? (int)((uint32_t)usage * 100u / (uint32_t)(cur * req))
-                             : (int)(((long long)usage * 100) / ((long long)cur * req));
-          const double nr = (double)nu / (double)target;
-          if ((tol_lo <= nr && nr <= tol_hi) || nr < 1.0) proposal = cur;
-          else proposal = max(cur, (int)ceil(nr * (double)cur));
-        } else if (tol_lo <= ratio && ratio <= tol_hi) {
-          proposal = cur;
-        } else {
-          proposal = (int)ceil(ratio * (double)ready);
+      const bool unready_up = cur > ready && util > target;  // ratio > 1 <=> util > target
+      if (unready_up || util < ulo || util > uhi) {
+        // the replica count the ratio asks for: ceil(ratio * base), with base =
+        // cur and ratio recomputed over every replica (unready ones idle) when
+        // unready pods exist and the load grows
+        int u = util, base = ready;
+        bool keep = false;
+        if (unready_up) {
+          const int dcur = cur * req;
+          if (__builtin_expect(usage >= 0 && usage <= 21474836 && cur <= 32767, 1))
+            u = fdiv_floor(usage * 100, dcur, __builtin_amdgcn_rcpf((float)dcur));
+          else
+            u = (int)(((long long)usage * 100) / ((long long)cur * req));
+          keep = (u >= ulo && u <= uhi) || u < target;  // within(nr) || nr < 1
+          base = cur;
+        }
+        if (!keep) {
+          int c;
+          if (__builtin_expect(u >= 0 && u <= 65535, 1)) {
+            const int x = u * base;  // < 2^31
+            const int q = fdiv_floor(x, target, rtarget);
+            c = q + (x != q * target ? 1 : 0);
+            if (x == q * target)  // exact multiple: the binary64 product may round above q
+              c = (int)ceil(((double)u / (double)target) * (double)base);
+          } else {
+            c = (int)ceil(((double)u / (double)target) * (double)base);
+          }
+          proposal = unready_up ? max(cur, c) : c;
         }
       }
     }
@@ -558,17 +593,25 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           a = __builtin_elementwise_min(a, as_s2(bfi((uint32_t)rup.stab16[w], hup[w], 0x7FFF7FFFu)));
         upr = min(upr, min((int)a.x, (int)a.y));
       }
-      {
+      int rc = max(cur, upr);
+      if (rc >= cur && (!BDEF || proposal < cur)) {  // BDEF: a scale-up proposal is its own max
         short2v a = as_s2(bfi(dn16[0], hdn[0], 0x80008000u));
 #pragma unroll
         for (int w = 1; w < 4; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
         dnr = max(dnr, max((int)a.x, (int)a.y));
+        rc = min(rc, dnr);
       }
-      int rc = max(cur, upr);
-      rc = min(rc, dnr);
       int lo = minr, hi = mx;
-      if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
-      else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+      if constexpr (BDEF) {
+        // up: max(Percent 100 -> ceil(2.0*cur), Pods 4 -> cur+4) over 15 s
+        // periods (no 60 s history inside), never below cur; down: Percent 100
+        // -> int(cur*0.0) = 0, never above cur
+        if (rc > cur) hi = min(hi, max(2 * cur, cur + 4));
+        else if (rc < cur) lo = max(lo, 0);
+      } else {
+        if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
+        else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+      }
       desired = rc < lo ? lo : (rc > hi ? hi : rc);
     }
     D1_STAMP(9);
@@ -576,27 +619,22 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     {
       const int rv = min(max(proposal, -D1_REC_SAT - 1), D1_REC_SAT);
       ring_push(hdn, ran ? rv : (int)0x8000);
-      ring_push(hup, ran ? rv : 0x7FFF);
+      if constexpr (!BDEF) {
+        ring_push(hup, ran ? rv : 0x7FFF);
+        ring_push(hdel, (hpa_path && desired != cur) ? desired - cur : 0);
+      }
     }
-    ring_push(hdel, (hpa_path && desired != cur) ? desired - cur : 0);
-    // Disruption is re-evaluated after a scale-DOWN only. A scale-up leaves
-    // every ready slot as it was unless pods land on one (scheduling pass 0
-    // marks that), lowers the PDB allowance (fewer candidates) and adds only
-    // in-flight slots or in-flight pods (readiness marks those), so an
-    // evaluation that found no deletion finds none again; a scale-down can
-    // raise the PDB allowance without moving a pod.
-    if (desired < cur) dirty = true;
     replicas = desired;
 
     D1_STAMP(2);
     // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
     if (placed > replicas) {
       int excess = placed - replicas;
-      dirty = true;
       placed = replicas;
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
+        if (!m || excess <= 0) continue;  // skipped by the wave when no lane needs the pass
         int removed = 0, removed_c = 0;
 #pragma unroll
         for (int n = MAXN - 1; n >= 0; --n) {  // branch-free: k = 0 leaves the slot untouched
@@ -605,13 +643,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           excess -= k;
           removed += k;
           if (pass == 1) removed_c += (cmask >> n & 1u) ? k : 0;
-          if (k > 0) {  // if-converted selects
-            slast[n] = t;
-            selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
-          }
+          slc[n] = k > 0 ? t + scas[n] : slc[n];
         }
-        // the cached energy sums cover ready slots only: pass 1 refreshes them
-        if (pass == 1) { rpods -= removed; Ffree += removed_c; acc_dirty = acc_dirty || removed > 0; }
+        if (pass == 1) { rpods -= removed; Ffree += removed_c; }
       }
     }
     // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
@@ -620,20 +654,19 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask;
+        if (!m || pd <= 0) continue;  // skipped by the wave when no lane needs the pass
         int added = 0;
 #pragma unroll
         for (int n = 0; n < MAXN; ++n) {  // branch-free first fit
-          const int k = (m >> n & 1u) ? max(min(scap[n] - spods[n], pd), 0) : 0;
+          const int fr = (m >> n & 1u) ? scap[n] - spods[n] : 0;
+          const int k = min(fr, pd);  // fr, pd >= 0
           spods[n] += k;
           pd -= k;
           added += k;
-          if (k > 0) {  // if-converted selects
-            slast[n] = t;
-            selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
-          }
+          slc[n] = k > 0 ? t + scas[n] : slc[n];
         }
         placed += added;
-        if (pass == 0 && added > 0) { rpods += added; Ffree -= added; dirty = true; acc_dirty = true; }
+        if (pass == 0) { rpods += added; Ffree -= added; }
       }
     }
     D1_STAMP(3);
@@ -658,21 +691,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             const int info = e.y, price = e.x;
             const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
             const int rs = t + delay;
-            const int el = max(rs, t + cq);
             const int4 ac = s_acc[bk];
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
               if (n == slot) {
-                sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13) | cas16(cq);
+                sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13);
                 sready[n] = rs;
-                slast[n] = t;
+                slc[n] = t + casc(cq);
+                scas[n] = casc(cq);
                 spods[n] = k;
                 sprice[n] = price;
                 scap[n] = cap1;
-                selig[n] = el;
                 sdyn[n] = (uint32_t)ac.z;
-                sinvf[n] = __builtin_amdgcn_rcpf((float)ac.w);
                 salloc[n] = ac.w;
+                sallocr[n] = delay == 0 ? ac.w : 0;
               }
             }
             const uint32_t bit = 1u << slot;
@@ -681,12 +713,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
             for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
             placed += k;
+            minscap = min(minscap, cap1);
             Isum += ((long long)ac.y << 32) | (unsigned)ac.x;  // idle draw from launch on
             if (delay == 0) {
               rdy |= bit;
               rpods += k;
-              dirty = true;
-              acc_dirty = true;
               if (cmask & bit) Ffree += cap1 - k;
             }
             else next_ready = min(next_ready, rs);
@@ -704,185 +735,145 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
 
     D1_STAMP(4);
-    // ---- G. disruption (only when state changed or a node became consolidatable) ----
-    if constexpr (STAMPS) st_acc[10] += __ballot(dirty || t >= wake) != 0 ? 1 : 0;
-    if ((dirty || t >= wake) && !(ablate & 1)) {
-      bool budget_hit = false, any_del = false;
-      // One branch-free pass: consolidatable (ready, idle >= consolidateAfter)
-      // slots, empty slots, the free capacity F of the compatible ready slots
-      // and the next wake-up step.
-      uint32_t eb[MAXN], mb[MAXN];
-      int wv[MAXN];
+    // ---- G. disruption (SEMANTICS §3.G) ----
+    // Candidates are the consolidatable slots (ready, idle >= consolidateAfter:
+    // t >= slc). A deletion needs an empty candidate, or a candidate of a
+    // WhenEmptyOrUnderutilized pool whose pods fit the other compatible ready
+    // slots (F minus its own free space >= its pods, i.e. F >= its capacity),
+    // which needs F >= the smallest node capacity. That gate costs a few
+    // instructions per slot; the exact sequential evaluation runs only in the
+    // lanes it admits (and only in waves where one does).
+    uint32_t elig = 0, emp = 0;
 #pragma unroll
-      for (int n = 0; n < MAXN; ++n) {  // independent per-slot terms, then pairwise trees
-        eb[n] = ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
-        mb[n] = spods[n] == 0 ? (1u << n) : 0u;
-        wv[n] = ((used >> n & 1u) && selig[n] > t) ? selig[n] : 0x7fffffff;
-      }
+    for (int n = MAXN - 1; n >= 0; --n) {  // slot masks built by doubling: 2 VALU per slot and mask
+      elig = 2 * elig + (slc[n] <= t ? 1u : 0u);
+      emp = 2 * emp + (spods[n] == 0 ? 1u : 0u);
+    }
+    elig &= rdy;
+    emp &= used;
+    uint32_t weou = 0;
 #pragma unroll
-      for (int w = MAXN / 2; w > 0; w >>= 1)
-#pragma unroll
-        for (int n = 0; n < w; ++n) {
-          eb[n] |= eb[n + w];
-          mb[n] |= mb[n + w];
-          wv[n] = min(wv[n], wv[n + w]);
-        }
-      uint32_t elig = eb[0];
-      const uint32_t empty_m = mb[0];
-      const int F = Ffree;
-      int wk = opqv(wv[0]);  // materialise now (the compiler would otherwise keep 8 compare masks alive)
+    for (int q = 0; q < MAXP; ++q)
+      if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) weou |= pmask[q];
+    const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)));
+    if constexpr (STAMPS) st_acc[10] += __ballot(gate != 0) != 0 ? 1 : 0;
+    if (gate && !(ablate & 1)) {
       // PDB evictions allowed (32-bit: pct <= 100 and replicas <= 32767)
       int allowed = 0x7fffffff;
       if (pdb_pct >= 0) {
         const int rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
         allowed = max(rdyp - (int)(((uint32_t)(pdb_pct * reps) + 99u) / 100u), 0);
       }
-      // WhenEmptyOrUnderutilized test of every slot (SEMANTICS §3.G): its pods
-      // fit on the other compatible ready slots (F minus its own free space)
-      // and the PDB allows evicting them
-      uint32_t ub[MAXN];
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        const int need = (cmask >> n & 1u) ? scap[n] : spods[n];
-        ub[n] = (need <= F && (!pdb_member || spods[n] <= allowed)) ? (1u << n) : 0u;
-      }
-#pragma unroll
-      for (int w = MAXN / 2; w > 0; w >>= 1)
-#pragma unroll
-        for (int n = 0; n < w; ++n) ub[n] |= ub[n + w];
-      const uint32_t under_m = ub[0];
-      uint32_t valid = 0;
+      bool any_del = false;
 #pragma unroll
       for (int q = 0; q < MAXP; ++q) {
         if (q >= NP) break;
-        valid |= elig & pmask[q] & (empty_m | (ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED ? under_m : 0u));
-        // ceil(budget% x nodes) <= 0 with nodes > 0  <=>  budget% <= 0
-        if (pmask[q] && budget[q] <= 0) budget_hit = true;
-      }
-      if (valid) {  // exact sequential evaluation (a deletion happens this step)
+        const int npool = __popc(pmask[q]);
+        if (npool == 0) continue;
+        const int qbudget = (budget[q] * npool + 99) / 100;
+        const bool weou_q = ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
+        int deleted = 0;
+        while (deleted < qbudget) {
+          const uint32_t cand = elig & pmask[q] & (weou_q ? ~0u : emp);
+          if (!cand) break;
+          // the first valid candidate in (pods asc, price desc, slot asc) order
+          unsigned long long bkey = ~0ull;
 #pragma unroll
-        for (int q = 0; q < MAXP; ++q) {
-          if (q >= NP) break;
-          const int npool = __popc(pmask[q]);
-          if (npool == 0) continue;
-          const int qbudget = (budget[q] * npool + 99) / 100;
-          int deleted = 0;
-          while (true) {
-            if (deleted >= qbudget) { budget_hit = true; break; }
-            const uint32_t cand = elig & pmask[q];
-            if (!cand) break;
-            int F = 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) if ((rdy & cmask) >> n & 1u) F += scap[n] - spods[n];
-            unsigned long long bkey = ~0ull;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              if (!(cand >> n & 1u)) continue;
-              const int pods = spods[n];
-              bool ok = pods == 0;
-              if (!ok && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) {
-                const int fo = F - ((cmask >> n & 1u) ? scap[n] - pods : 0);
-                ok = fo >= pods && (!pdb_member || pods <= allowed);
-              }
-              const unsigned long long key = (unsigned long long)pods << 36 |
-                                             (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
-              if (ok && key < bkey) bkey = key;
-            }
-            if (bkey == ~0ull) break;
-            const int best = (int)(bkey & 15u), bpods = (int)(bkey >> 36);
-            // move the candidate's pods first-fit onto the other compatible ready nodes
+          for (int n = 0; n < MAXN; ++n) {
+            const int pods = spods[n];
+            const int need = (cmask >> n & 1u) ? scap[n] : pods;  // F counts its own free space
+            const bool ok = (cand >> n & 1u) &&
+                            (pods == 0 || (need <= Ffree && (!pdb_member || pods <= allowed)));
+            const unsigned long long key = (unsigned long long)pods << 36 |
+                                           (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
+            if (ok && key < bkey) bkey = key;
+          }
+          if (bkey == ~0ull) break;
+          const int best = (int)(bkey & 15u), bpods = (int)(bkey >> 36);
+          if (bpods > 0) {
+            // move its pods first-fit onto the other compatible ready nodes
             int need = bpods;
             const uint32_t recv = rdy & cmask & ~(1u << best);
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
-              if (need > 0 && (recv >> n & 1u)) {
-                const int k = min(scap[n] - spods[n], need);
-                if (k > 0) {
-                  spods[n] += k;
-                  need -= k;
-                  slast[n] = t;
-                  selig[n] = max(sready[n], t + (int)(sinfo[n] >> 16));
-                }
-              }
+              const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
+              const int k = min(fr, need);
+              spods[n] += k;
+              need -= k;
+              slc[n] = k > 0 ? t + scas[n] : slc[n];
             }
-            // delete the node (its pods moved between ready nodes: running counts unchanged)
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              if (n == best) {
-                if ((sinfo[n] >> 12 & 1u) == 0) nsp--; else nod--;
-                burn -= sprice[n];
-                const int4 ac = s_acc[sinfo[n] & 1023u];
-                Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
-                sdyn[n] = 0;
-                sinvf[n] = 0.f;
-                salloc[n] = 0;
-                sinfo[n] = 0; sready[n] = 0; slast[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
-                selig[n] = 0;
-              }
-            }
-            const uint32_t nb = ~(1u << best);
-            used &= nb; rdy &= nb; cmask &= nb; pmask[q] &= nb;
-            if (pdb_member) allowed -= bpods;
-            deleted++;
-            deletions++;
-            any_del = true;
-            acc_dirty = true;
-            flags |= 4u;
-            elig = 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) elig |= ((rdy >> n & 1u) && t >= selig[n]) ? (1u << n) : 0u;
           }
+          // delete the node (its pods moved between ready nodes: running counts unchanged)
+          uint32_t binfo = 0;
+          int bcap = 0, bprice = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (n == best) {
+              binfo = sinfo[n];
+              bcap = scap[n];
+              bprice = sprice[n];
+              sallocr[n] = 0;
+              spods[n] = 0;
+            }
+          }
+          if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
+          burn -= bprice;
+          const int4 ac = s_acc[binfo & 1023u];
+          Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
+          // F loses the node's free space and the moved pods: its whole capacity
+          if ((rdy & cmask) >> best & 1u) Ffree -= bcap;
+          else Ffree -= bpods;
+          const uint32_t nb = ~(1u << best);
+          used &= nb; rdy &= nb; cmask &= nb;
+#pragma unroll
+          for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
+          if (pdb_member) allowed -= bpods;
+          deleted++;
+          deletions++;
+          any_del = true;
+          flags |= 4u;
+          // receivers may have become ineligible, the node is gone
+          elig = 0;
+          emp &= nb;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            elig |= slc[n] <= t ? (1u << n) : 0u;
+            emp &= spods[n] == 0 ? ~0u : ~(1u << n);
+          }
+          elig &= rdy;
         }
       }
-      dirty = budget_hit || any_del;
-      if (any_del) {
-        Ffree = 0;
+      if (any_del) {  // capacity of the remaining nodes
+        minscap = 0x7fffffff;
 #pragma unroll
-        for (int n = 0; n < MAXN; ++n) Ffree += ((rdy & cmask) >> n & 1u) ? scap[n] - spods[n] : 0;  // slots changed: next step at which a node becomes consolidatable
-        wk = 0x7fffffff;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) if ((used >> n & 1u) && selig[n] > t) wk = min(wk, selig[n]);
+        for (int n = 0; n < MAXN; ++n) minscap = (used >> n & 1u) ? min(minscap, scap[n]) : minscap;
       }
-      wake = wk;
     }
 
     D1_STAMP(5);
-    // ---- H. accounting ----
-    if (acc_dirty) {  // branch-free refresh of the cached sums (I is kept incrementally)
-      acc_dirty = false;
-      long long sv[MAXN];
-      float rv[MAXN];
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        const int pr = (rdy >> n & 1u) ? spods[n] : 0;
-        sv[n] = (long long)((unsigned long long)sdyn[n] * (unsigned)pr);
-        rv[n] = (float)pr * sinvf[n];
-      }
-#pragma unroll
-      for (int w = MAXN / 2; w > 0; w >>= 1)  // pairwise trees: short dependency chains
-#pragma unroll
-        for (int n = 0; n < w; ++n) { sv[n] += sv[n + w]; rv[n] = fmaxf(rv[n], rv[n + w]); }
-      Ssum = sv[0];
-      Rmax = rv[0];
-    }
+    // ---- H. accounting (SEMANTICS §3.H, exact integer nanowatt-minutes) ----
+    // per node use = min(pods * upp, alloc) with sallocr = 0 on nodes not
+    // ready; pods < 2^15 and upp < 2^16 keep every product in 32 bits
     int upp = 0;
     if (rpods > 0) {
       const long long rcap = (long long)rpods * limit;
-      const int usage = (limit > 0 && rcap < (long long)L) ? (int)rcap : L;
-      upp = (int)((uint32_t)max(usage, 0) / (uint32_t)rpods);
+      const int usage = max((limit > 0 && rcap < (long long)L) ? (int)rcap : L, 0);
+      upp = fdiv_floor(usage, rpods, __builtin_amdgcn_rcpf((float)rpods));
     }
-    long long e_step;
-    if ((float)upp * Rmax < 0.9999f && !(ablate & 4)) {
-      e_step = base_nw + Isum + (long long)((unsigned long long)(uint32_t)upp * (unsigned long long)Ssum);
-    } else {  // a node saturates (use clamped at its allocatable CPU): branch-free,
-              // 24-bit products (pods < 2^15, clamped upp < 2^24, alloc < 2^24)
-      e_step = base_nw + Isum;
-      const uint32_t uc = (uint32_t)min(upp, 0xFFFFFF);
+    long long e_step = base_nw + Isum;
+    if (__builtin_expect(upp <= 0xFFFF, 1)) {
+      unsigned long long ed = 0;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] & 0x7FFFu : 0u;
-        const uint64_t prod = (uint64_t)pr * (uint64_t)uc;
-        const uint32_t al = (uint32_t)salloc[n] & 0xFFFFFFu;
+        const uint32_t use = min(__umul24((uint32_t)spods[n], (uint32_t)upp), (uint32_t)sallocr[n]);
+        ed += (unsigned long long)sdyn[n] * use;
+      }
+      e_step += (long long)ed;
+    } else {
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const uint64_t prod = (uint64_t)(uint32_t)spods[n] * (uint64_t)(uint32_t)upp;
+        const uint32_t al = (uint32_t)sallocr[n];
         const uint32_t use = prod < (uint64_t)al ? (uint32_t)prod : al;
         e_step += (long long)((uint64_t)sdyn[n] * use);
       }
@@ -899,7 +890,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     D1_STAMP(6);
     rec_prev = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16,
                          (step_last_type & 0xFFFF) | (int)(flags << 16));
-    Lcur = opqv(Lraw);
+#pragma unroll
+    for (int k = 0; k + 1 < D1_PF; ++k) Lq[k] = Lq[k + 1];
+    Lq[D1_PF - 1] = opqv(Lraw);
   }
   if (traj) *(int4*)(traj + (int64_t)(T - 1) * ls + i) = rec_prev;
   D1_STAMP(7);
@@ -936,8 +929,7 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const int64_t waves = (p.N + p.lpw - 1) / p.lpw;
   const unsigned grid = (unsigned)((waves + B / WAVE - 1) / (B / WAVE));
   const size_t lds = (size_t)p.K * sizeof(int4);
-  // OCC = resident waves per SIMD the register allocation targets: 2 (no
-  // spills); 3 is a diagnostic instantiation (spills, measured slower)
+  // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
   if (p.stamps) {
     if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, p);
