@@ -214,6 +214,7 @@ static int d1_check_world(ccka_ctx* c) {
   for (int q = 0; q < w.n_pools; ++q)
     if (w.pools[q].limit_cpu_m >= 0) return CCKA_OK;
   if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
+      dp.limit_cpu_m > 65535 ||
       dp.min_replicas < 0 || dp.max_replicas < 0 || dp.max_replicas > D1_REC_SAT || dp.replicas0 > D1_REC_SAT)
     return CCKA_OK;
   // 32-bit PDB arithmetic (pct x replicas) and pending-pod-minutes (pods x steps)

@@ -227,15 +227,16 @@ __device__ __forceinline__ short2v as_s2(uint32_t x) { return __builtin_bit_cast
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
 // floor(a / b) for 0 <= a < 2^31, 1 <= b < 2^30, given rb = 1/(float)b
-// (v_rcp_f32): the f32 estimate is within one of the quotient while the
-// quotient is below 2^20, and one remainder test corrects it; larger
-// quotients take the exact integer division (a branch no real input takes).
-__device__ __forceinline__ int fdiv_floor(int a, int b, float rb) {
+// (v_rcp_f32), without a branch: the f32 estimate is within one of the
+// quotient while the quotient is below 2^20, and one remainder test corrects
+// it. `bad` is set when those preconditions fail (the caller then recomputes
+// exactly); lanes whose inputs are meaningless get a meaningless quotient and
+// no fault.
+__device__ __forceinline__ int fdiv_nb(int a, int b, float rb, bool& bad) {
   int q = (int)((float)a * rb);
-  if (__builtin_expect(q >= (1 << 20) || b >= (1 << 30), 0)) return a / b;
-  // remainder in [-b, 2b): exact in 32-bit two's complement
   const int r = (int)((uint32_t)a - (uint32_t)q * (uint32_t)b);
   q += (r >= b ? 1 : 0) - (r < 0 ? 1 : 0);
+  bad = bad || (uint32_t)q >= (1u << 20) || (uint32_t)b >= (1u << 30);
   return q;
 }
 
@@ -331,7 +332,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int K = opq(p.K), Z = opq(p.Z), T = opq(p.T);
   const int ps = opq(p.peak_start), pe = opq(p.peak_end);
   const long long base_nw = opq(p.base_nw), ls = opq(p.N);
-  const double tol_lo = opq(p.tol_lo), tol_hi = opq(p.tol_hi);
   const GLOBAL_AS int32_t* const price = opq_ptr(p.price);
   const GLOBAL_AS double* const ci_gpwmin = opq_ptr(p.ci_gpwmin);
   const GLOBAL_AS int2* const table = opq_ptr(p.table);
@@ -524,67 +524,55 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 
     D1_STAMP(1);
     // ---- C. HPA (replica_calculator.go + horizontal.go, SEMANTICS §3.C) ----
+    // Straight-line in every lane (some lane of a wave has a scale event on
+    // nearly every step, so branches would only add exec-mask traffic).
     // util = int32(usage*100 / (ready*req)) by an f32-reciprocal division with
     // an exact remainder correction; the tolerance band, the unready rule and
     // the SLO threshold are integer tests on util (exactly the binary64 tests
-    // of the spec, see ulo/uhi). The proposal ceil(fl(fl(util/target)*ready))
-    // equals the exact integer ceiling unless util*ready is a multiple of
-    // target (|rounding error| < 1/target otherwise); only that case runs the
-    // binary64 expression.
+    // of the spec, see ulo/uhi). The proposal ceil(fl(fl(u/target)*base))
+    // equals the exact integer ceiling unless u*base is a multiple of target
+    // (|rounding error| < 1/target otherwise); only that case, and inputs
+    // beyond the fast arithmetic's range, run the spec's expression (rare
+    // branches).
     const int cur = replicas, ready = rpods;
-    int desired = cur, proposal = cur, util = 0;
-    bool ran = false, hpa_path = true, util_valid = false;
-    if (cur == 0 && minr != 0) {
-      hpa_path = false;
-    } else if (cur > mx) {
-      desired = mx;
-    } else if (cur < minr) {
-      desired = minr;
-    } else if (ready > 0) {
-      const long long rcap = (long long)ready * limit;
-      const int usage = (limit > 0 && rcap < (long long)L) ? (int)rcap : L;
-      const int dreq = ready * req;  // < 2^31: ready <= 32767, req <= 65535
-      if (__builtin_expect(usage >= 0 && usage <= 21474836, 1))
-        util = fdiv_floor(usage * 100, dreq, __builtin_amdgcn_rcpf((float)dreq));
-      else
-        util = (int)(((long long)usage * 100) / ((long long)dreq));
-      util_valid = true;
-      ran = true;
+    const bool metric = cur <= mx && cur >= minr && ready > 0 && !(cur == 0 && minr != 0);
+    int util = 0, proposal = cur;
+    {
+      const int rcapv = ready * limit;  // limit <= 65535 (d1_check_world)
+      const int usage = (limit > 0 && rcapv < L) ? rcapv : L;
+      const int a = usage * 100;
+      const int dreq = ready * req;     // < 2^31: ready <= 32767, req <= 65535
+      const int dcur = cur * req;
+      bool slow = usage < 0 || usage > 21474836;
+      util = fdiv_nb(a, dreq, __builtin_amdgcn_rcpf((float)dreq), slow);
+      const int nu = fdiv_nb(a, dcur, __builtin_amdgcn_rcpf((float)dcur), slow);
+      if (__builtin_expect(metric && slow, 0))  // exact 64-bit quotient
+        util = (int)(((long long)usage * 100) / ((long long)ready * req));
       const bool unready_up = cur > ready && util > target;  // ratio > 1 <=> util > target
-      if (unready_up || util < ulo || util > uhi) {
-        // the replica count the ratio asks for: ceil(ratio * base), with base =
-        // cur and ratio recomputed over every replica (unready ones idle) when
-        // unready pods exist and the load grows
-        int u = util, base = ready;
-        bool keep = false;
-        if (unready_up) {
-          const int dcur = cur * req;
-          if (__builtin_expect(usage >= 0 && usage <= 21474836 && cur <= 32767, 1))
-            u = fdiv_floor(usage * 100, dcur, __builtin_amdgcn_rcpf((float)dcur));
-          else
-            u = (int)(((long long)usage * 100) / ((long long)cur * req));
-          keep = (u >= ulo && u <= uhi) || u < target;  // within(nr) || nr < 1
-          base = cur;
-        }
-        if (!keep) {
-          int c;
-          if (__builtin_expect(u >= 0 && u <= 65535, 1)) {
-            const int x = u * base;  // < 2^31
-            const int q = fdiv_floor(x, target, rtarget);
-            c = q + (x != q * target ? 1 : 0);
-            if (x == q * target)  // exact multiple: the binary64 product may round above q
-              c = (int)ceil(((double)u / (double)target) * (double)base);
-          } else {
-            c = (int)ceil(((double)u / (double)target) * (double)base);
-          }
-          proposal = unready_up ? max(cur, c) : c;
-        }
-      }
+      int u = util, base = ready;
+      if (unready_up) { u = nu; base = cur; }  // every replica counted, unready ones idle
+      if (__builtin_expect(metric && slow && unready_up, 0))
+        u = (int)(((long long)usage * 100) / ((long long)cur * req));
+      const bool keep = (u >= ulo && u <= uhi) || (unready_up && u < target);  // within || nr < 1
+      bool slow2 = (uint32_t)u > 0xFFFFu;
+      const int x = u * base;  // < 2^31 when u <= 0xFFFF
+      const int q = fdiv_nb(x, target, rtarget, slow2);
+      const bool exactm = x == q * target;
+      int c = q + (exactm ? 0 : 1);
+      if (__builtin_expect(metric && !keep && (exactm || slow2), 0))  // binary64 as the spec writes it
+        c = (int)ceil(((double)u / (double)target) * (double)base);
+      const int pe = unready_up ? max(cur, c) : c;
+      proposal = (metric && !keep) ? pe : cur;
     }
+    const bool ran = metric;
+    const bool hpa_path = !(cur == 0 && minr != 0);
+    const bool util_valid = metric;
     D1_STAMP(8);
     if constexpr (STAMPS) st_acc[11] += __ballot(ran && proposal != cur) != 0 ? 1 : 0;
-    if (ran && proposal != cur && !(ablate & 8)) {
-      // stabilisation: packed min / max over the records inside each window
+    // stabilisation (packed min / max over the records inside each window) and
+    // the rate limits; desired == cur exactly when proposal == cur
+    int desired = cur > mx ? mx : (cur < minr && hpa_path ? minr : cur);
+    {
       int upr = proposal, dnr = proposal;
       if (rup.stab_mask) {  // wave-uniform
         short2v a = as_s2(bfi((uint32_t)rup.stab16[0], hup[0], 0x7FFF7FFFu));
@@ -593,26 +581,28 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           a = __builtin_elementwise_min(a, as_s2(bfi((uint32_t)rup.stab16[w], hup[w], 0x7FFF7FFFu)));
         upr = min(upr, min((int)a.x, (int)a.y));
       }
-      int rc = max(cur, upr);
-      if (rc >= cur && (!BDEF || proposal < cur)) {  // BDEF: a scale-up proposal is its own max
+      {
         short2v a = as_s2(bfi(dn16[0], hdn[0], 0x80008000u));
 #pragma unroll
         for (int w = 1; w < 4; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
         dnr = max(dnr, max((int)a.x, (int)a.y));
-        rc = min(rc, dnr);
       }
+      int rc = min(max(cur, upr), dnr);
       int lo = minr, hi = mx;
       if constexpr (BDEF) {
         // up: max(Percent 100 -> ceil(2.0*cur), Pods 4 -> cur+4) over 15 s
         // periods (no 60 s history inside), never below cur; down: Percent 100
         // -> int(cur*0.0) = 0, never above cur
-        if (rc > cur) hi = min(hi, max(2 * cur, cur + 4));
-        else if (rc < cur) lo = max(lo, 0);
+        hi = rc > cur ? min(hi, max(2 * cur, cur + 4)) : hi;
+        lo = rc < cur ? max(lo, 0) : lo;
       } else {
-        if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
-        else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+        if (ran && proposal != cur) {
+          if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
+          else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+        }
       }
-      desired = rc < lo ? lo : (rc > hi ? hi : rc);
+      const int db = rc < lo ? lo : (rc > hi ? hi : rc);
+      if (ran && !(ablate & 8)) desired = db;
     }
     D1_STAMP(9);
     // records clamp to int16 (replicas stay in [0, 32767]; min/max commute with clamping)
@@ -855,10 +845,13 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     // per node use = min(pods * upp, alloc) with sallocr = 0 on nodes not
     // ready; pods < 2^15 and upp < 2^16 keep every product in 32 bits
     int upp = 0;
-    if (rpods > 0) {
-      const long long rcap = (long long)rpods * limit;
-      const int usage = max((limit > 0 && rcap < (long long)L) ? (int)rcap : L, 0);
-      upp = fdiv_floor(usage, rpods, __builtin_amdgcn_rcpf((float)rpods));
+    {
+      const int rcapv = rpods * limit;
+      const int usage = max((limit > 0 && rcapv < L) ? rcapv : L, 0);
+      bool slow = false;
+      upp = fdiv_nb(usage, max(rpods, 1), __builtin_amdgcn_rcpf((float)rpods), slow);
+      if (__builtin_expect(slow, 0)) upp = usage / max(rpods, 1);
+      upp = rpods > 0 ? upp : 0;
     }
     long long e_step = base_nw + Isum;
     if (__builtin_expect(upp <= 0xFFFF, 1)) {
