@@ -764,55 +764,69 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         const bool weou_q = ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
         int deleted = 0;
         while (deleted < qbudget) {
-          const uint32_t cand = elig & pmask[q] & (weou_q ? ~0u : emp);
-          if (!cand) break;
-          // the first valid candidate in (pods asc, price desc, slot asc) order
-          unsigned long long bkey = ~0ull;
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            const int pods = spods[n];
-            const int need = (cmask >> n & 1u) ? scap[n] : pods;  // F counts its own free space
-            const bool ok = (cand >> n & 1u) &&
-                            (pods == 0 || (need <= Ffree && (!pdb_member || pods <= allowed)));
-            const unsigned long long key = (unsigned long long)pods << 36 |
-                                           (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
-            if (ok && key < bkey) bkey = key;
-          }
-          if (bkey == ~0ull) break;
-          const int best = (int)(bkey & 15u), bpods = (int)(bkey >> 36);
-          if (bpods > 0) {
-            // move its pods first-fit onto the other compatible ready nodes
-            int need = bpods;
-            const uint32_t recv = rdy & cmask & ~(1u << best);
+          const uint32_t cand = elig & pmask[q];
+          const uint32_t ce = cand & emp;
+          if (!ce && !(weou_q && (cand & ~emp) && (Ffree >= minscap || (cand & ~emp & ~cmask)))) break;
+          int best = -1, bpods = 0, bprice = -1, bcap = 0;
+          uint32_t binfo = 0;
+          if (ce) {
+            // empty candidates come first (pods asc): the highest price, then
+            // the lowest slot; deleting one moves nothing
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
-              const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
-              const int k = min(fr, need);
-              spods[n] += k;
-              need -= k;
-              slc[n] = k > 0 ? t + scas[n] : slc[n];
+              const bool c = (ce >> n & 1u) && sprice[n] > bprice;
+              best = c ? n : best;
+              bprice = c ? sprice[n] : bprice;
+              bcap = c ? scap[n] : bcap;
+              binfo = c ? sinfo[n] : binfo;
+            }
+          } else {
+            // under-utilised candidates (pods asc, price desc, slot asc), valid
+            // when their pods fit the other compatible ready slots (F minus
+            // their own free space) and the PDB allows evicting them
+            unsigned long long bkey = ~0ull;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              const int pods = spods[n];
+              const int need = (cmask >> n & 1u) ? scap[n] : pods;
+              const bool ok = (cand >> n & 1u) && need <= Ffree && (!pdb_member || pods <= allowed);
+              const unsigned long long key = (unsigned long long)pods << 36 |
+                                             (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
+              const bool c = ok && key < bkey;
+              bkey = c ? key : bkey;
+              bcap = c ? scap[n] : bcap;
+              binfo = c ? sinfo[n] : binfo;
+            }
+            if (bkey != ~0ull) {
+              best = (int)(bkey & 15u);
+              bpods = (int)(bkey >> 36);
+              bprice = 0x7fffffff - (int)((bkey >> 4) & 0x7fffffffull);
+              // move its pods first-fit onto the other compatible ready nodes
+              int need = bpods;
+              const uint32_t recv = rdy & cmask & ~(1u << best);
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
+                const int k = min(fr, need);
+                spods[n] += k;
+                need -= k;
+                slc[n] = k > 0 ? t + scas[n] : slc[n];
+              }
             }
           }
+          if (best < 0) break;
           // delete the node (its pods moved between ready nodes: running counts unchanged)
-          uint32_t binfo = 0;
-          int bcap = 0, bprice = 0;
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
-            if (n == best) {
-              binfo = sinfo[n];
-              bcap = scap[n];
-              bprice = sprice[n];
-              sallocr[n] = 0;
-              spods[n] = 0;
-            }
+            sallocr[n] = n == best ? 0 : sallocr[n];
+            spods[n] = n == best ? 0 : spods[n];
           }
           if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
           burn -= bprice;
           const int4 ac = s_acc[binfo & 1023u];
           Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
           // F loses the node's free space and the moved pods: its whole capacity
-          if ((rdy & cmask) >> best & 1u) Ffree -= bcap;
-          else Ffree -= bpods;
+          Ffree -= ((rdy & cmask) >> best & 1u) ? bcap : bpods;
           const uint32_t nb = ~(1u << best);
           used &= nb; rdy &= nb; cmask &= nb;
 #pragma unroll
@@ -822,15 +836,18 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           deletions++;
           any_del = true;
           flags |= 4u;
-          // receivers may have become ineligible, the node is gone
-          elig = 0;
+          elig &= nb;
           emp &= nb;
+          if (bpods > 0) {  // receivers got pods (and a new consolidatable-from step)
+            uint32_t el = 0, em = 0;
 #pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            elig |= slc[n] <= t ? (1u << n) : 0u;
-            emp &= spods[n] == 0 ? ~0u : ~(1u << n);
+            for (int n = MAXN - 1; n >= 0; --n) {
+              el = 2 * el + (slc[n] <= t ? 1u : 0u);
+              em = 2 * em + (spods[n] == 0 ? 1u : 0u);
+            }
+            elig = el & rdy;
+            emp = em & used;
           }
-          elig &= rdy;
         }
       }
       if (any_del) {  // capacity of the remaining nodes
