@@ -288,7 +288,20 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 // takes well under an HBM miss, and every in-step vector-memory wait (the
 // argmin-table row of a launch, the hourly price tile) also waits for all
 // older loads still in flight.
+#ifndef D1_PF_OVERRIDE
 constexpr int D1_PF = 3;
+#else
+constexpr int D1_PF = D1_PF_OVERRIDE;
+#endif
+
+// build-time variants of the single-deployment kernel (tools/variants.sh
+// compares them; the shipped build uses the defaults)
+#ifndef D1_V_ACC
+#define D1_V_ACC 0  // 0: per-node exact energy every step; 1: cached sums refreshed on change
+#endif
+#ifndef D1_V_NU
+#define D1_V_NU 1   // 1: the unready-pods utilisation only in lanes with unready pods
+#endif
 
 template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
@@ -389,10 +402,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
   int salloc[MAXN];     // alloc_cpu_m of the slot's type (< 2^24 by eligibility)
   int sallocr[MAXN];    // salloc once the node is ready, else 0
+  float sinv[MAXN];     // 1/alloc (saturation pre-test of D1_V_ACC 1)
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
     sinfo[n] = 0; sready[n] = 0; slc[n] = 0; scas[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
-    sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0;
+    sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0; sinv[n] = 0.f;
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
   const uint32_t slot_mask = maxn >= 32 ? 0xFFFFFFFFu : ((1u << maxn) - 1u);
@@ -420,6 +434,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   long long cost = 0, burn = 0, base_price = 0;
   int pend_min = 0;  // <= 32767 pods x T steps
   long long energy_nw = 0, e_hour = 0, Isum = 0;  // exact nanowatt-minutes; Isum: idle draw of used slots
+  unsigned long long Ssum = 0;  // D1_V_ACC 1: sum over ready slots of dyn_nw_per_m * pods
+  float Rmax = 0.f;             // D1_V_ACC 1: max over ready slots of pods/alloc
+  bool acc_dirty = false;
   double gco2 = 0.0, ci_min = 0.0;
   int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
   uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
@@ -489,6 +506,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             rdy |= 1u << n;
             rpods += spods[n];
             sallocr[n] = salloc[n];
+            acc_dirty = true;
             if (cmask >> n & 1u) Ffree += scap[n] - spods[n];
           }
           else next_ready = min(next_ready, sready[n]);
@@ -545,7 +563,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       const int dcur = cur * req;
       bool slow = usage < 0 || usage > 21474836;
       util = fdiv_nb(a, dreq, __builtin_amdgcn_rcpf((float)dreq), slow);
+#if D1_V_NU
+      int nu = 0;
+      if (cur > ready) nu = fdiv_nb(a, dcur, __builtin_amdgcn_rcpf((float)dcur), slow);
+#else
       const int nu = fdiv_nb(a, dcur, __builtin_amdgcn_rcpf((float)dcur), slow);
+#endif
       if (__builtin_expect(metric && slow, 0))  // exact 64-bit quotient
         util = (int)(((long long)usage * 100) / ((long long)ready * req));
       const bool unready_up = cur > ready && util > target;  // ratio > 1 <=> util > target
@@ -635,7 +658,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           if (pass == 1) removed_c += (cmask >> n & 1u) ? k : 0;
           slc[n] = k > 0 ? t + scas[n] : slc[n];
         }
-        if (pass == 1) { rpods -= removed; Ffree += removed_c; }
+        if (pass == 1) { rpods -= removed; Ffree += removed_c; acc_dirty = acc_dirty || removed > 0; }
       }
     }
     // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
@@ -656,7 +679,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           slc[n] = k > 0 ? t + scas[n] : slc[n];
         }
         placed += added;
-        if (pass == 0) { rpods += added; Ffree -= added; }
+        if (pass == 0) { rpods += added; Ffree -= added; acc_dirty = acc_dirty || added > 0; }
       }
     }
     D1_STAMP(3);
@@ -695,6 +718,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 sdyn[n] = (uint32_t)ac.z;
                 salloc[n] = ac.w;
                 sallocr[n] = delay == 0 ? ac.w : 0;
+                sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
               }
             }
             const uint32_t bit = 1u << slot;
@@ -708,6 +732,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             if (delay == 0) {
               rdy |= bit;
               rpods += k;
+              acc_dirty = true;
               if (cmask & bit) Ffree += cap1 - k;
             }
             else next_ready = min(next_ready, rs);
@@ -835,6 +860,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           deleted++;
           deletions++;
           any_del = true;
+          acc_dirty = true;
           flags |= 4u;
           elig &= nb;
           emp &= nb;
@@ -860,7 +886,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     D1_STAMP(5);
     // ---- H. accounting (SEMANTICS §3.H, exact integer nanowatt-minutes) ----
     // per node use = min(pods * upp, alloc) with sallocr = 0 on nodes not
-    // ready; pods < 2^15 and upp < 2^16 keep every product in 32 bits
+    // ready; pods < 2^15 and upp < 2^16 keep every product in 32 bits (all
+    // operands uint32: a mixed int/unsigned min() resolves to the double overload)
     int upp = 0;
     {
       const int rcapv = rpods * limit;
@@ -870,12 +897,33 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       if (__builtin_expect(slow, 0)) upp = usage / max(rpods, 1);
       upp = rpods > 0 ? upp : 0;
     }
+#if D1_V_ACC == 1
+    if (acc_dirty) {  // ready pods changed: refresh the cached sums
+      acc_dirty = false;
+      unsigned long long sv = 0;
+      float rv = 0.f;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] : 0u;
+        sv += (unsigned long long)sdyn[n] * pr;
+        rv = fmaxf(rv, (float)pr * sinv[n]);
+      }
+      Ssum = sv;
+      Rmax = rv;
+    }
+    const bool fast_e = (float)upp * Rmax < 0.9999f;  // no node saturates
+#else
+    const bool fast_e = false;
+    (void)Rmax; (void)sinv; (void)acc_dirty;
+#endif
     long long e_step = base_nw + Isum;
-    if (__builtin_expect(upp <= 0xFFFF, 1)) {
+    if (fast_e) {
+      e_step += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+    } else if (__builtin_expect(upp <= 0xFFFF, 1)) {
       unsigned long long ed = 0;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        const uint32_t use = min(__umul24((uint32_t)spods[n], (uint32_t)upp), (uint32_t)sallocr[n]);
+        const uint32_t use = min((uint32_t)spods[n] * (uint32_t)upp, (uint32_t)sallocr[n]);  // both uint32: v_min_u32
         ed += (unsigned long long)sdyn[n] * use;
       }
       e_step += (long long)ed;

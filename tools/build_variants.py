@@ -1,0 +1,28 @@
+"""Build-time variants of the single-deployment kernel (D1_V_* macros in
+rollout_d1.hip) as separate libccka.so copies under csrc/build/variants/<name>/,
+linked with the main build's other objects. Profiling aid only.
+usage: python tools/build_variants.py name=-DD1_V_ACC=1 [name2="-DA -DB" ...]"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc")
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+         "-Wall", "-Wno-unused-function"]
+subprocess.run(["make", "-s", "-C", CSRC], check=True)
+procs = []
+for arg in sys.argv[1:]:
+    name, _, defs = arg.partition("=")
+    out = os.path.join(CSRC, "build", "variants", name)
+    os.makedirs(out, exist_ok=True)
+    obj = os.path.join(out, "rollout_d1.o")
+    procs.append((name, out, obj, subprocess.Popen(["/opt/rocm/bin/hipcc", *FLAGS, *defs.split(), "-c", "-o", obj,
+                                                    os.path.join(CSRC, "rollout_d1.hip")])))
+for name, out, obj, p in procs:
+    assert p.wait() == 0, name
+    others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "sweep.o", "mlp.o", "ccka_abi.o")]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                    os.path.join(out, "libccka.so"), obj, *others, "-L/opt/rocm/lib", "-lrccl",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    print("built", name)
