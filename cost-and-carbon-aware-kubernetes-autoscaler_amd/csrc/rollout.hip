@@ -461,7 +461,16 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     ninfo[n] = 0; nready[n] = 0; nlast[n] = 0; nprice[n] = 0; ncap[n] = 0; nsrc[n] = 0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) npods[n][d] = 0;
-  }
+  }  // slots tainted karpenter.sh/disrupted: sources of an in-flight pre-spun
+  // replacement and those replacements (SEMANTICS 3.G0/G2)
+  auto taint_mask = [&]() {
+    uint32_t m = 0;
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n)
+      if (nsrc[n]) m |= (1u << n) | (1u << (nsrc[n] - 1));
+    return m;
+  };
+
   uint32_t used = 0, rdy = 0;
   const uint32_t slot_mask = NN >= 32 ? 0xFFFFFFFFu : ((1u << NN) - 1u);
   int next_ready = 0x7fffffff;  // earliest ready_step among not-ready nodes
@@ -711,6 +720,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         }
       }
       // ---- E. kube-scheduler (ready) / F1. nomination (in-flight) ----
+      // nodes tainted karpenter.sh/disrupted (a source whose pre-spun
+      // replacement is in flight, and that replacement) take no other pods
+      const uint32_t tnt = (greplace || gdrift) ? taint_mask() : 0u;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d >= D) break;
@@ -718,7 +730,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         if (pd > 0) {
 #pragma unroll
           for (int pass = 0; pass < 2; ++pass) {
-            const uint32_t m = pass == 0 ? rdy : (used & ~rdy);
+            const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & ~tnt;
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
               const uint32_t x = ninfo[n];
@@ -952,6 +964,39 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             }
           }
         };
+        // the F2 launch rule for one NodeClaim, per lane (SEMANTICS 3.F): spot
+        // offerings only when spot is allowed and any is feasible; argmin of
+        // (score, k, z, c), score = price + carbon weight * 1000 * p_ref_w * ci
+        auto lane_launch = [&](uint32_t zm, uint32_t cm, int use, int limit, int s_cpu, int s_mem, int s_pods,
+                               int& bk, int& bz, int& bc, int& bpr) {
+          bk = -1; bz = 0; bc = 0; bpr = 0;
+          bool spot_only = false;
+          if (cm & CCKA_CAP_SPOT) {
+            for (int k = 0; k < L.K && !spot_only; ++k) {
+              if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
+              if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+              for (int z = 0; z < L.Z; ++z)
+                if ((zm >> z & 1u) && tprice(L, rl, k, z, 0) > 0) { spot_only = true; break; }
+            }
+          }
+          double bs = 0.0;
+          for (int k = 0; k < L.K; ++k) {
+            if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
+            if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+            const double carbon = L.types[k].p_ref_w * ci_gpwh;
+            for (int z = 0; z < L.Z; ++z) {
+              if (!(zm >> z & 1u)) continue;
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                if (!(cm & capbit(c)) || (spot_only && c != 0)) continue;
+                const int pr = tprice(L, rl, k, z, c);
+                if (pr <= 0) continue;
+                const double score = (double)pr + wc1000 * carbon;
+                if (bk < 0 || score < bs) { bk = k; bz = z; bc = c; bpr = pr; bs = score; }
+              }
+            }
+          }
+        };
         // a pre-spun replacement node for slot `src` (no pods until it takes over)
         auto launch_replacement = [&](int q, int slot, int src, int bk, int bz, int bc, int bpr) {
           const bool now_ready = delay == 0;
@@ -1156,7 +1201,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               if (pdb_pods > allowed) continue;
               // pods move first-fit onto ready, non-drifted nodes; the rest are
               // evicted (Pending until E/F of a later step)
-              const uint32_t recv = rdy & ~dmask;
+              const uint32_t recv = rdy & ~dmask & ~taint_mask();
               int left[DMAX];
 #pragma unroll
               for (int d = 0; d < DMAX; ++d) {
@@ -1206,7 +1251,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               }
               const uint32_t fr = ~used & slot_mask;
               int bk = -1, bz = 0, bc = 0, bpr = 0;
-              if (s_pods > 0 && fr && cm) find_offer(zm, cm, use, limit, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
+              // an ordinary provisioning decision: the F2 launch rule
+              if (s_pods > 0 && fr && cm) lane_launch(zm, cm, use, limit, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
               if (bk >= 0) {
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n)
@@ -1249,6 +1295,11 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             }
             pm &= used;
             cm1 &= used;
+            {
+              const uint32_t tn = taint_mask();
+              pm &= ~tn;   // no source of an in-flight replacement is a candidate
+              cm1 &= ~tn;  // nor a receiver of moved pods
+            }
             while (true) {
               if (deleted >= budget) { budget_hit = true; break; }
               int F = 0;
@@ -1304,7 +1355,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             if (greplace && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
             continue;
           }
-          uint32_t rejected = 0;
+          uint32_t rejected = taint_mask();  // tainted nodes: neither candidates nor receivers
+          const uint32_t tn_g = rejected;
           while (true) {
             if (deleted >= budget) { budget_hit = true; break; }
             int best = -1, bpods = 0, bprice = 0;
@@ -1332,7 +1384,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                 int free_sum = 0;
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n)
-                  if (n != best && (rdy >> n & 1u) && (capbit(ni_cap(ninfo[n])) & capsel[0]))
+                  if (n != best && ((rdy & ~tn_g) >> n & 1u) && (capbit(ni_cap(ninfo[n])) & capsel[0]))
                     free_sum += ncap[n] - npods[n][0];
                 if (free_sum < bpods) ok = false;
               }
@@ -1340,7 +1392,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               int need_d = bpods;
 #pragma unroll
               for (int n = 0; n < MAXN; ++n) {
-                if (need_d > 0 && n != best && (rdy >> n & 1u) && (capbit(ni_cap(ninfo[n])) & capsel[0])) {
+                if (need_d > 0 && n != best && ((rdy & ~tn_g) >> n & 1u) && (capbit(ni_cap(ninfo[n])) & capsel[0])) {
                   const int k = min(ncap[n] - npods[n][0], need_d);
                   if (k > 0) { npods[n][0] += k; need_d -= k; nlast[n] = t; }
                 }
@@ -1371,7 +1423,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
                   for (int n = 0; n < MAXN; ++n) {
                     const uint32_t x = ninfo[n];
-                    if (need_d > 0 && n != best && (rdy >> n & 1u) && (capbit(ni_cap(x)) & capsel[d])) {
+                    if (need_d > 0 && n != best && ((rdy & ~tn_g) >> n & 1u) && (capbit(ni_cap(x)) & capsel[d])) {
                       int sc = 0, sm = 0, sp = 0;
 #pragma unroll
                       for (int e = 0; e < DMAX; ++e) {

@@ -82,6 +82,7 @@ static bool looks_number(const std::string& s) {
     else if ((c == 'e' || c == 'E') && digit && !exp) {
       exp = true;
       if (i + 1 < s.size() && (s[i + 1] == '-' || s[i + 1] == '+')) ++i;
+      if (i + 1 >= s.size()) return false;  // "1e", "1e+": no exponent digits
     } else return false;
   }
   return digit;
@@ -118,7 +119,32 @@ struct JsonParser {
   void ws() {
     while (i < s.size() && std::isspace((unsigned char)s[i])) ++i;
   }
-  std::string str() {
+  static void utf8(std::string& out, unsigned cp) {
+    if (cp < 0x80) out += (char)cp;
+    else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 63)); }
+    else if (cp < 0x10000) {
+      out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 63)); out += (char)(0x80 | (cp & 63));
+    } else {
+      out += (char)(0xF0 | (cp >> 18)); out += (char)(0x80 | ((cp >> 12) & 63));
+      out += (char)(0x80 | ((cp >> 6) & 63)); out += (char)(0x80 | (cp & 63));
+    }
+  }
+  unsigned hex(int n) {
+    if (i + (size_t)n > s.size()) err("bad hex escape");
+    unsigned v = 0;
+    for (int d = 0; d < n; ++d) {
+      const char h = s[i++];
+      v <<= 4;
+      if (h >= '0' && h <= '9') v |= (unsigned)(h - '0');
+      else if (h >= 'a' && h <= 'f') v |= (unsigned)(h - 'a' + 10);
+      else if (h >= 'A' && h <= 'F') v |= (unsigned)(h - 'A' + 10);
+      else err("bad hex escape");
+    }
+    return v;
+  }
+  // a double-quoted string; `yaml` adds YAML 1.1's extra escapes (\0 \a \v \e
+  // \xHH \UHHHHHHHH \N \_ \L \P, escaped space) to JSON's
+  std::string str(bool yaml = false) {
     if (s[i] != '"') err("expected string");
     ++i;
     std::string out;
@@ -133,16 +159,35 @@ struct JsonParser {
           case 'r': out += '\r'; break;
           case 'b': out += '\b'; break;
           case 'f': out += '\f'; break;
+          case '"': case '\\': case '/': out += e; break;
           case 'u': {
-            if (i + 4 > s.size()) err("bad \\u");
-            unsigned cp = (unsigned)std::strtoul(s.substr(i, 4).c_str(), nullptr, 16);
-            i += 4;
-            if (cp < 0x80) out += (char)cp;
-            else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 63)); }
-            else { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 63)); out += (char)(0x80 | (cp & 63)); }
+            unsigned cp = hex(4);
+            if (cp >= 0xD800 && cp < 0xDC00 && i + 6 <= s.size() && s[i] == '\\' && s[i + 1] == 'u') {
+              const size_t save = i;
+              i += 2;
+              const unsigned lo = hex(4);
+              if (lo >= 0xDC00 && lo < 0xE000) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+              else i = save;
+            }
+            utf8(out, cp);
             break;
           }
-          default: out += e;
+          default:
+            if (!yaml) err("bad escape");
+            switch (e) {
+              case '0': out += '\0'; break;
+              case 'a': out += '\a'; break;
+              case 'v': out += '\v'; break;
+              case 'e': out += '\x1b'; break;
+              case ' ': case '\t': out += e; break;
+              case 'x': utf8(out, hex(2)); break;
+              case 'U': utf8(out, hex(8)); break;
+              case 'N': utf8(out, 0x85); break;
+              case '_': utf8(out, 0xA0); break;
+              case 'L': utf8(out, 0x2028); break;
+              case 'P': utf8(out, 0x2029); break;
+              default: err("bad escape");
+            }
         }
       } else {
         out += c;
@@ -276,34 +321,73 @@ struct Line {
   int no;
 };
 
-std::string strip_comment(const std::string& s) {
-  bool sq = false, dq = false;
+// YAML quotes and flow brackets only open at the start of a scalar: after
+// nothing, an open bracket or comma of an enclosing flow collection, or a
+// ': ' / '- ' / '? ' indicator. Anywhere else ("0\"", "a[0]", "it's") they
+// are plain characters. Calls f(k, depth) for every character outside quotes
+// (depth = open flow brackets); f returns true to stop the scan. Returns the
+// quote character when the text ends inside a quoted scalar (it continues on
+// the next line), else 0.
+template <class F>
+static char yaml_scan(const std::string& s, F&& f) {
+  int depth = 0;
+  auto token_start = [&](size_t k, auto&& self) -> bool {
+    size_t p = k;
+    while (p > 0 && (s[p - 1] == ' ' || s[p - 1] == '\t')) --p;
+    if (p == 0) return true;
+    const char c = s[p - 1];
+    if (c == '[' || c == '{') return depth > 0;
+    if (c == ',') return depth > 0;
+    if ((c == ':' || c == '-' || c == '?') && p < k) return c == ':' || self(p - 1, self);
+    return false;
+  };
   for (size_t k = 0; k < s.size(); ++k) {
     const char c = s[k];
-    if (c == '\'' && !dq) sq = !sq;
-    else if (c == '"' && !sq) dq = !dq;
-    else if (c == '#' && !sq && !dq && (k == 0 || std::isspace((unsigned char)s[k - 1]))) return s.substr(0, k);
+    if ((c == '\'' || c == '"') && token_start(k, token_start)) {
+      size_t j = k + 1;
+      for (; j < s.size(); ++j) {
+        if (c == '"' && s[j] == '\\') { ++j; continue; }
+        if (s[j] == c) {
+          if (c == '\'' && j + 1 < s.size() && s[j + 1] == '\'') { ++j; continue; }
+          break;
+        }
+      }
+      if (j >= s.size()) return c;  // unterminated: continues on the next line
+      k = j;  // the closing quote
+      continue;
+    }
+    if (c == '[' || c == '{') {
+      if (depth > 0 || token_start(k, token_start)) ++depth;
+    } else if ((c == ']' || c == '}') && depth > 0) {
+      --depth;
+    }
+    if (f(k, depth)) return 0;
   }
-  return s;
+  return 0;
+}
+
+static char open_quote(const std::string& s) {
+  return yaml_scan(s, [](size_t, int) { return false; });
+}
+
+std::string strip_comment(const std::string& s) {
+  size_t cut = std::string::npos;
+  yaml_scan(s, [&](size_t k, int) {
+    if (s[k] == '#' && (k == 0 || std::isspace((unsigned char)s[k - 1]))) { cut = k; return true; }
+    return false;
+  });
+  return cut == std::string::npos ? s : s.substr(0, cut);
 }
 
 // position of the ':' that ends a mapping key, or npos
 size_t key_colon(const std::string& s) {
-  bool sq = false, dq = false;
-  int depth = 0;
-  for (size_t k = 0; k < s.size(); ++k) {
-    const char c = s[k];
-    if (c == '\'' && !dq) sq = !sq;
-    else if (c == '"' && !sq) dq = !dq;
-    else if (!sq && !dq) {
-      if (c == '[' || c == '{') ++depth;
-      else if (c == ']' || c == '}') --depth;
-      else if (c == ':' && depth == 0 && (k + 1 == s.size() || s[k + 1] == ' ' || s[k + 1] == '\t'))
-        return k;
-    }
-    if (k == 0 && (c == '[' || c == '{')) return std::string::npos;  // flow collection scalar
-  }
-  return std::string::npos;
+  if (!s.empty() && (s[0] == '[' || s[0] == '{')) return std::string::npos;  // flow collection scalar
+  size_t at = std::string::npos;
+  yaml_scan(s, [&](size_t k, int depth) {
+    if (s[k] == ':' && depth == 0 && (k + 1 == s.size() || s[k + 1] == ' ' || s[k + 1] == '\t')) { at = k; return true; }
+    return false;
+  });
+  return at;
 }
 
 bool is_dash(const std::string& s) { return s == "-" || (s.size() >= 2 && s[0] == '-' && s[1] == ' '); }
@@ -324,7 +408,7 @@ struct FlowParser {
     if (i < s.size() && s[i] == '"') {
       JsonParser jp(s);
       jp.i = i;
-      std::string t = jp.str();
+      std::string t = jp.str(true);
       i = jp.i;
       return Value::str(t);
     }
@@ -472,10 +556,35 @@ struct YamlParser {
 };
 }  // namespace
 
+// bracket depth of a flow collection's text (quotes skipped): > 0 while it
+// continues on the next line (emitters wrap long flow collections)
+static int flow_depth(const std::string& s) {
+  int depth = 0;
+  yaml_scan(s, [&](size_t, int d) { depth = d; return false; });
+  return depth;
+}
+
+// the value part of a block line that starts a flow collection, else ""
+static std::string flow_start(const std::string& t) {
+  std::string v;
+  if (!t.empty() && (t[0] == '[' || t[0] == '{')) v = t;
+  else if (is_dash(t)) v = trim(t.substr(1));
+  else {
+    const size_t c = key_colon(t);
+    if (c != std::string::npos) v = trim(t.substr(c + 1));
+  }
+  if (!v.empty() && (v[0] == '[' || v[0] == '{')) return v;
+  if (is_dash(t) && !v.empty() && v != t) return flow_start(v);  // "- key: [..." or "- - [..."
+  return std::string();
+}
+
 std::vector<Value> parse_yaml_documents(const std::string& text) {
   std::vector<std::vector<Line>> docs(1);
   size_t start = 0;
   int no = 0;
+  int pend_depth = 0;  // open brackets of a flow collection continued on the next line
+  char pend_quote = 0;  // quote of a quoted scalar continued on the next line
+  int pend_blank = 0;   // empty lines inside that scalar so far
   while (start <= text.size()) {
     size_t end = text.find('\n', start);
     if (end == std::string::npos) end = text.size();
@@ -486,14 +595,52 @@ std::vector<Value> parse_yaml_documents(const std::string& text) {
     if (raw.find('\t') != std::string::npos && raw.find_first_not_of(" \t") != std::string::npos &&
         raw[raw.find_first_not_of(' ')] == '\t')
       throw ParseError("yaml line " + std::to_string(no) + ": tab indentation");
+    if (pend_quote) {  // line folding inside a multi-line quoted scalar (YAML 1.1 7.3)
+      const std::string t = trim(raw);
+      if (t.empty()) {
+        ++pend_blank;
+        if (end == text.size()) break;
+        continue;
+      }
+      std::string& acc = docs.back().back().text;
+      size_t bs = 0;
+      while (bs < acc.size() && acc[acc.size() - 1 - bs] == '\\') ++bs;
+      if (pend_quote == '"' && (bs & 1)) {  // escaped line break: joined without a space
+        acc.pop_back();
+        acc += std::string((size_t)pend_blank, '\n');
+      } else {
+        while (!acc.empty() && (acc.back() == ' ' || acc.back() == '\t')) acc.pop_back();
+        acc += pend_blank ? std::string((size_t)pend_blank, '\n') : std::string(" ");
+      }
+      pend_blank = 0;
+      acc += t;
+      pend_quote = open_quote(acc);
+      if (!pend_quote) {
+        acc = trim(strip_comment(acc));
+        const std::string fv = flow_start(acc);
+        pend_depth = fv.empty() ? 0 : std::max(0, flow_depth(fv));
+      }
+      if (end == text.size()) break;
+      continue;
+    }
     const std::string body = strip_comment(raw);
     const std::string t = trim(body);
+    if (pend_depth > 0 && !t.empty()) {  // continuation of a wrapped flow collection
+      docs.back().back().text += " " + t;
+      pend_depth = std::max(0, flow_depth(flow_start(docs.back().back().text)));
+      pend_quote = open_quote(docs.back().back().text);
+      if (end == text.size()) break;
+      continue;
+    }
     if (t.empty()) { if (end == text.size()) break; continue; }
     if (t == "---" || t.rfind("--- ", 0) == 0) { docs.emplace_back(); continue; }
     if (t == "...") continue;
     int ind = 0;
     while (ind < (int)body.size() && body[(size_t)ind] == ' ') ++ind;
     docs.back().push_back({ind, trim(body), no});
+    const std::string fv = flow_start(docs.back().back().text);
+    if (!fv.empty()) pend_depth = std::max(0, flow_depth(fv));
+    pend_quote = open_quote(docs.back().back().text);
     if (end == text.size()) break;
   }
   std::vector<Value> out;

@@ -355,6 +355,45 @@ static int o_offer(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, int64
   return bk;
 }
 
+/* The launch choice of a NodeClaim with sums (sc, sm, sp) (SEMANTICS 3.F):
+ * candidates hold the sums, fit the pool limit and have an offering with
+ * z in zm, c in cm, price > 0; if spot is allowed and any spot offering is
+ * feasible only spot offerings compete; the lexicographic minimum of
+ * (score, k, z, c), score = price + carbon_weight*1000*(p_ref_w*ci). -1 if none. */
+static int o_launch_choice(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, int64_t use, int32_t limit,
+                           int64_t sc, int64_t sm, int64_t sp, double wc1000, int* bz, int* bc, int32_t* bp) {
+  const ccka_world* w = e->w;
+  int spot_only = 0;
+  if (cm & CCKA_CAP_SPOT) {
+    for (int k = 0; k < e->K && !spot_only; ++k) {
+      const ccka_itype* ty = &w->types[k];
+      if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, sc, sm, sp, 0, 0) < 0) continue;
+      if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+      for (int z = 0; z < e->Z; ++z)
+        if ((zm >> z & 1u) && o_price(e, r, h, k, z, 0) > 0) { spot_only = 1; break; }
+    }
+  }
+  int bk = -1;
+  double bs = 0.0;
+  for (int k = 0; k < e->K; ++k) {
+    const ccka_itype* ty = &w->types[k];
+    if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, sc, sm, sp, 0, 0) < 0) continue;
+    if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+    for (int z = 0; z < e->Z; ++z) {
+      if (!(zm >> z & 1u)) continue;
+      for (int cc = 0; cc < 2; ++cc) {
+        if (!(cm & (uint32_t)o_capidx_bit(cc))) continue;
+        if (spot_only && cc != 0) continue;
+        const int32_t pr = o_price(e, r, h, k, z, cc);
+        if (pr <= 0) continue;
+        const double score = (double)pr + wc1000 * (ty->p_ref_w * w->ci_gpwh[r * 24 + h]);
+        if (bk < 0 || score < bs) { bk = k; *bz = z; *bc = cc; *bp = pr; bs = score; }
+      }
+    }
+  }
+  return bk;
+}
+
 /* a pre-spun replacement for slot src, no pods until it takes over */
 static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, int ready, int t, int src) {
   o_node* nd = &st->nodes[slot];
@@ -372,6 +411,17 @@ static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, 
   st->hash = (st->hash ^ st->last_choice) * 16777619u;
 }
 
+/* Karpenter taints a disruption candidate karpenter.sh/disrupted:NoSchedule
+ * while its replacement is in flight: neither the source nor the pre-spun
+ * replacement (sized for the source's pods, SEMANTICS 3.G0/G2) receives other
+ * pods until the takeover, and the source is no consolidation candidate. */
+static int o_tainted(const o_node* nodes, int NN, int n) {
+  if (nodes[n].src1) return 1;
+  for (int m = 0; m < NN; ++m)
+    if (nodes[m].used && nodes[m].src1 == n + 1) return 1;
+  return 0;
+}
+
 static int o_drifted(const o_state* st, const o_node* nd) {
   const o_pool* pl = &st->pools[nd->pool];
   return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
@@ -380,7 +430,7 @@ static int o_drifted(const o_state* st, const o_node* nd) {
 static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* load, int64_t i,
                       int64_t nsc, ccka_results* out, ccka_traj_rec* traj) {
   const ccka_world* w = e->w;
-  const int D = e->D, NN = e->N, K = e->K;
+  const int D = e->D, NN = e->N;
   o_state st;
   memset(&st, 0, sizeof st);
   /* load column: the scenario's own trace, or its shared trace (policy sweeps) */
@@ -559,6 +609,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           const int rdy = nd->ready_step <= t;
           if ((pass == 0 && !rdy) || (pass == 1 && rdy)) continue;
           if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
+          if (o_tainted(st.nodes, NN, n)) continue;
           const int64_t f = o_node_fit(e, nd, d);
           const int k = (int)(f < p ? f : p);
           if (k > 0) { nd->pods[d] += k; p -= k; nd->last_event = t; }
@@ -632,34 +683,10 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       for (int c = 0; c < ncl; ++c) {
         o_claim* cl = &claims[c];
         const int32_t limit = w->pools[cl->pool].limit_cpu_m;
-        int spot_only = 0;
-        if (cl->cap & CCKA_CAP_SPOT) {
-          for (int k = 0; k < K && !spot_only; ++k) {
-            const ccka_itype* ty = &w->types[k];
-            if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, cl->s_cpu, cl->s_mem, cl->s_pods, 0, 0) < 0) continue;
-            if (limit >= 0 && pool_use[cl->pool] + (int64_t)ty->vcpu * 1000 > limit) continue;
-            for (int z = 0; z < e->Z; ++z)
-              if ((cl->zone >> z & 1u) && o_price(e, r, h, k, z, 0) > 0) { spot_only = 1; break; }
-          }
-        }
-        int bk = -1, bz = 0, bc = 0;
-        double bs = 0.0;
-        for (int k = 0; k < K; ++k) {
-          const ccka_itype* ty = &w->types[k];
-          if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, cl->s_cpu, cl->s_mem, cl->s_pods, 0, 0) < 0) continue;
-          if (limit >= 0 && pool_use[cl->pool] + (int64_t)ty->vcpu * 1000 > limit) continue;
-          for (int z = 0; z < e->Z; ++z) {
-            if (!(cl->zone >> z & 1u)) continue;
-            for (int cc = 0; cc < 2; ++cc) {
-              if (!(cl->cap & (uint32_t)o_capidx_bit(cc))) continue;
-              if (spot_only && cc != 0) continue;
-              const int32_t pr = o_price(e, r, h, k, z, cc);
-              if (pr <= 0) continue;
-              const double score = (double)pr + wc1000 * (ty->p_ref_w * w->ci_gpwh[r * 24 + h]);
-              if (bk < 0 || score < bs) { bk = k; bz = z; bc = cc; bs = score; }
-            }
-          }
-        }
+        int bz = 0, bc = 0;
+        int32_t bpr = 0;
+        const int bk = o_launch_choice(e, r, h, cl->zone, cl->cap, pool_use[cl->pool], limit, cl->s_cpu, cl->s_mem,
+                                       cl->s_pods, wc1000, &bz, &bc, &bpr);
         if (bk < 0) { continue; /* dropped: slot stays free */ }
         o_node* nd = &st.nodes[cl->slot];
         memset(nd, 0, sizeof *nd);
@@ -740,6 +767,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
             for (int m = 0; m < NN && need > 0; ++m) {
               o_node* nd = &st.nodes[m];
               if (m == n || !nd->used || nd->ready_step > t || o_drifted(&st, nd)) continue;
+              if (o_tainted(st.nodes, NN, m)) continue;
               if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
               const int64_t f = o_node_fit(e, nd, d);
               const int k = (int)(f < need ? f : need);
@@ -766,8 +794,9 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
               if (st.nodes[m].used && st.nodes[m].pool == p) use += (int64_t)w->types[st.nodes[m].type].vcpu * 1000;
             int bz = 0, bc = 0, bk = -1;
             int32_t bp = 0;
-            if (sp > 0 && slot >= 0 && cm)
-              bk = o_offer(e, r, h, st.pools[p].zone_mask, cm, use, w->pools[p].limit_cpu_m, sc, sm, sp, &bz, &bc, &bp);
+            if (sp > 0 && slot >= 0 && cm)  /* an ordinary provisioning decision: the F2 rule */
+              bk = o_launch_choice(e, r, h, st.pools[p].zone_mask, cm, use, w->pools[p].limit_cpu_m, sc, sm, sp,
+                                   wc1000, &bz, &bc, &bp);
             if (bk >= 0) {
               for (int d = 0; d < D; ++d) dn->pods[d] = left[d];
               o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, n);
@@ -792,6 +821,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
             const o_node* nd = &st.nodes[n];
             if (!nd->used || nd->pool != p || nd->ready_step > t || rejected[n]) continue;
             if ((int64_t)(t - nd->last_event) * CCKA_STEP_SECONDS < st.pools[p].ca_s) continue;
+            if (o_tainted(st.nodes, NN, n)) continue;
             int pods = 0;
             for (int d = 0; d < D; ++d) pods += nd->pods[d];
             if (pods > 0 && st.pools[p].policy != CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) continue;
@@ -813,6 +843,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
               for (int n = 0; n < NN && need > 0; ++n) {
                 o_node* nd = &trial[n];
                 if (n == best || !nd->used || nd->ready_step > t) continue;
+                if (o_tainted(trial, NN, n)) continue;
                 if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
                 const int64_t f = o_node_fit(e, nd, d);
                 const int k = (int)(f < need ? f : need);

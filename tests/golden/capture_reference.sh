@@ -28,9 +28,11 @@ run_variant() {   # run_variant <name> <script> [VAR=value ...]
   local work; work="$(mktemp -d /tmp/ccka_refcap.XXXXXX)"
   cp "$REF"/demo_00_env.sh "$REF/$script" "$work/"
   rm -f /tmp/np_req_*.json
+  # the script's status is recorded, not trapped by set -e
+  local rc=0
   ( cd "$work" && env -i HOME="$HOME" PATH="$STUBS:/usr/bin:/bin" CAPTURE_DIR="$cap" \
-      RESET_KILL_PF=false "$@" bash "./$script" > "$cap/stdout.txt" 2> "$cap/stderr.txt" )
-  echo "$?" > "$cap/exit_code"
+      RESET_KILL_PF=false "$@" bash "./$script" > "$cap/stdout.txt" 2> "$cap/stderr.txt" ) || rc=$?
+  echo "$rc" > "$cap/exit_code"
   rm -f "$cap/.seq" /tmp/np_req_*.json
   rm -rf "$work"
 }

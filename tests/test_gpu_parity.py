@@ -309,7 +309,14 @@ def test_drift_parity_single_deployment(engine, variant):
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
     assert engine.last_engine()[0] == 1  # drift runs on the general kernel
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
-    assert ((tc["flags"] & 16) != 0).any()  # drift deletions happened
+    f = tc["flags"]
+    # both drift branches are covered: a pre-spun replacement (flags 16|32) where
+    # a slot is free, and the eviction fallback (flags 16|4)
+    if variant != "one_slot":
+        assert ((f & 48) == 48).any()
+    else:
+        assert not ((f & 48) == 48).any()
+    assert ((f & 20) == 20).any()
     compare(rg, rc, tg, tc)
 
 
@@ -328,7 +335,7 @@ def test_drift_parity_multi_deployment(engine):
     load = po.gen_load(configs.trace_gen(9), spec.n_steps, 3, n)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
-    assert ((tc["flags"] & 16) != 0).any()
+    assert ((tc["flags"] & 48) == 48).any() and ((tc["flags"] & 20) == 20).any()
     compare(rg, rc, tg, tc)
 
 

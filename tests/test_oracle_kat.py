@@ -405,3 +405,26 @@ def test_replacement_consolidation_on_demand_to_cheaper():
     spec.price[0, 0, :, :, 0] = np.where(v[:, None] == 8, spec.price[0, 0, :, :, 0], 0)
     r2, _ = run(spec, load)
     assert r2["launches"][0] == 1 and r2["deletions"][0] == 0
+
+
+def test_drift_replacement_in_flight_is_tainted():
+    """karpenter.sh/disrupted (SEMANTICS 3.G0): 5 HPA pods run
+    on one spot node in us-east-2a; PEAK at t=10 drifts it and a replacement
+    sized for those 5 pods launches in us-east-2c (ready at t=12, delay 2). At
+    t=11 the HPA doubles the deployment. The 5 new pods must not land on the
+    tainted source nor be nominated onto the in-flight replacement: they form
+    a claim of their own, and the takeover at t=12 moves exactly the 5 source
+    pods, evicting none (running = replicas from t=13 on)."""
+    d = deployment(abi.SCALER_HPA, replicas0=5, min_r=1, max_r=20, target=50, limit_cpu=0)
+    spec = tiny_world([d], T=30, start_minute=950, pdb_pct=-1, drift=1, provision_delay_steps=2)
+    load = np.full((30, 1, 1), 500, np.int32)  # 5 pods x 200m at 50 %: in band
+    load[11:, 0, 0] = 1000                      # 100 %: ratio 2 -> 10 replicas at t=11
+    r, tr = run(spec, load)
+    reps, pend, fl = tr["replicas"][:, 0], tr["pending"][:, 0], tr["flags"][:, 0]
+    assert reps[10] == 5 and reps[11] == 10
+    assert (fl[10] & 16) and (fl[10] & 32)          # drift at t=10: pre-spun replacement
+    assert fl[11] & 2                               # the new pods get a claim of their own
+    assert fl[12] & 4 and not (fl[12] & 16)         # takeover: the source goes
+    assert pend[11] == 5 and pend[12] == 5          # only the new pods wait (claim ready at t=13)
+    assert (pend[13:] == 0).all()
+    assert r["launches"][0] == 3 and r["deletions"][0] == 1
