@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 STEP_SECONDS = 60
 MAX_TYPES = 1024
 MAX_ZONES = 4
@@ -121,6 +121,33 @@ class GridStats(C.Structure):
                 ("slo_minutes", C.c_int64), ("gco2", C.c_double), ("energy_wmin", C.c_double)]
 
 
+class Detail(C.Structure):
+    """ccka_detail: per-pool / base-group / per-deployment breakdown (ccka_set_detail)."""
+    _fields_ = [("pool_cost_uphmin", C.c_int64 * MAX_POOLS), ("pool_energy_nwmin", C.c_int64 * MAX_POOLS),
+                ("pool_gco2", C.c_double * MAX_POOLS), ("pool_node_min_spot", C.c_int32 * MAX_POOLS),
+                ("pool_node_min_od", C.c_int32 * MAX_POOLS), ("pool_final_nodes", C.c_int32 * MAX_POOLS),
+                ("pool_peak_nodes", C.c_int32 * MAX_POOLS), ("pool_launches", C.c_int32 * MAX_POOLS),
+                ("desired", C.c_int32 * MAX_DEPLOY), ("ready", C.c_int32 * MAX_DEPLOY),
+                ("pending", C.c_int32 * MAX_DEPLOY), ("base_cost_uphmin", C.c_int64),
+                ("base_energy_nwmin", C.c_int64), ("base_gco2", C.c_double)]
+
+
+def detail_dtype():
+    """numpy structured dtype laid out exactly as ccka_detail (arrays of it are
+    passed to ccka_get_detail / the oracle as a flat buffer)."""
+    import numpy as np
+    kinds = {C.c_int64: "<i8", C.c_int32: "<i4", C.c_double: "<f8"}
+    fields = []
+    for name, ct in Detail._fields_:
+        if hasattr(ct, "_length_"):
+            fields.append((name, kinds[ct._type_], (ct._length_,)))
+        else:
+            fields.append((name, kinds[ct]))
+    dt = np.dtype(fields)
+    assert dt.itemsize == C.sizeof(Detail)
+    return dt
+
+
 class TraceGen(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("base_lo", C.c_int32), ("base_hi", C.c_int32),
                 ("amp_lo_pm", C.c_int32), ("amp_hi_pm", C.c_int32), ("noise_pm", C.c_int32),
@@ -129,7 +156,7 @@ class TraceGen(C.Structure):
 
 
 STRUCT_ORDER = [ItType, Pool, Deployment, World, Scenarios, Results, TrajRec, Totals, TraceGen,
-                GridStats]
+                GridStats, Detail]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ENGINE_LIB = os.path.join(os.path.dirname(PKG_DIR), "csrc", "build", "libccka.so")
@@ -182,6 +209,8 @@ def load_engine(path: str | None = None):
         "ccka_get_results": (C.c_int, [vp, C.POINTER(Results)]),
         "ccka_get_trajectory": (C.c_int, [vp, C.POINTER(TrajRec), C.c_int64]),
         "ccka_get_totals": (C.c_int, [vp, C.POINTER(Totals)]),
+        "ccka_set_detail": (C.c_int, [vp, C.c_int32]),
+        "ccka_get_detail": (C.c_int, [vp, C.c_void_p, C.c_int64]),
         "ccka_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "ccka_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
         "ccka_allreduce_totals": (C.c_int, [vp, C.POINTER(Totals)]),
@@ -204,7 +233,7 @@ EXPORTED = [
     "ccka_get_trajectory", "ccka_get_totals", "ccka_comm_unique_id", "ccka_comm_init",
     "ccka_allreduce_totals", "ccka_comm_info", "ccka_device_info", "ccka_get_grid_stats", "ccka_pareto_frontier",
     "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
-    "ccka_mlp_forward_async", "ccka_mlp_get_actions",
+    "ccka_mlp_forward_async", "ccka_mlp_get_actions", "ccka_set_detail", "ccka_get_detail",
 ]
 
 

@@ -101,6 +101,16 @@ class Engine:
         self._chk(self.lib.ccka_get_totals(self.ctx, C.byref(t)), "ccka_get_totals")
         return t
 
+    def set_detail(self, on: bool = True):
+        """Record the per-pool / base-group / per-deployment breakdown
+        (ccka_detail) in later rollouts (the summary path)."""
+        self._chk(self.lib.ccka_set_detail(self.ctx, int(bool(on))), "ccka_set_detail")
+
+    def detail(self) -> np.ndarray:
+        a = np.zeros(self.n, abi.detail_dtype())
+        self._chk(self.lib.ccka_get_detail(self.ctx, a.ctypes.data, a.size), "ccka_get_detail")
+        return a
+
     # ---- policy sweep (config 4) ----
     def grid_stats(self, grid_size: int) -> np.ndarray:
         ng = self.n // grid_size

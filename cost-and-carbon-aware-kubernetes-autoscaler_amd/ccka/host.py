@@ -34,7 +34,10 @@ def lib():
             "ccka_host_build_world": (C.c_int, [vp, C.c_char_p, C.c_int32, C.c_int32,
                                                 C.POINTER(abi.World)]),
             "ccka_host_summary": (C.c_int, [vp, C.POINTER(abi.World), C.POINTER(abi.Results),
-                                            C.POINTER(abi.TrajRec), C.c_char_p, C.c_int64]),
+                                            C.POINTER(abi.TrajRec), C.c_void_p, C.c_char_p, C.c_int64]),
+            "ccka_host_label": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int32]),
+            "ccka_host_export_detail": (C.c_int, [vp, C.POINTER(abi.World), C.c_void_p, C.c_int64, C.c_int64,
+                                                  C.c_int64, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]),
             "ccka_host_export": (C.c_int, [vp, C.c_int32, C.POINTER(abi.World), C.POINTER(abi.TrajRec),
                                            C.c_int64, C.POINTER(abi.Results), C.c_int64, C.c_int64,
                                            C.c_int64, C.c_int64, C.c_char_p, C.c_int64,
@@ -53,7 +56,8 @@ def lib():
 HOST_EXPORTED = ["ccka_host_open", "ccka_host_close", "ccka_host_last_error", "ccka_host_apply",
                  "ccka_host_patch", "ccka_host_get_json", "ccka_host_policy_patch",
                  "ccka_host_burst_manifest", "ccka_host_build_world", "ccka_host_summary",
-                 "ccka_host_export", "ccka_host_set_admission", "ccka_host_admission_review"]
+                 "ccka_host_export", "ccka_host_set_admission", "ccka_host_admission_review",
+                 "ccka_host_label", "ccka_host_export_detail"]
 
 # Kyverno guard policies (04_kyverno.sh:24-75), ccka_host.h CCKA_ADMIT_*
 ADMIT_REQUIRE_REQUESTS_LIMITS = 1
@@ -130,10 +134,33 @@ class Host:
             self._err("build_world")
         return w
 
-    def summary(self, world, results, traj=None) -> str:
+    def label(self, kind, name, labels: str, overwrite=True):
+        """kubectl label <kind> <name> k=v ... [--overwrite] ("k-" removes)."""
+        if self.L.ccka_host_label(self.h, kind.encode(), name.encode(), labels.encode(), int(overwrite)) != 0:
+            self._err("label")
+
+    def summary(self, world, results, traj=None, detail=None) -> str:
+        """demo_41 summary of scenario 0; `detail` = ccka_detail records (abi.detail_dtype())."""
         tp = traj.ctypes.data_as(C.POINTER(abi.TrajRec)) if traj is not None else None
-        return self._str(self.L.ccka_host_summary(self.h, C.byref(world), C.byref(results), tp,
+        if detail is not None:
+            import numpy as np
+            detail = np.ascontiguousarray(detail, abi.detail_dtype())
+        dp = detail.ctypes.data if detail is not None else None
+        return self._str(self.L.ccka_host_summary(self.h, C.byref(world), C.byref(results), tp, dp,
                                                   self._buf, len(self._buf)), "summary")
+
+    def export_detail(self, world, detail, first_id=0, start_unix_ms=0) -> str:
+        """Per-pool Prometheus series of the ccka_detail records (ccka_host_export_detail)."""
+        import numpy as np
+        detail = np.ascontiguousarray(detail, abi.detail_dtype())
+        need = C.c_int64(0)
+        args = (self.h, C.byref(world), detail.ctypes.data, detail.size, first_id, start_unix_ms)
+        if self.L.ccka_host_export_detail(*args, None, 0, C.byref(need)) != 0 and need.value <= 0:
+            self._err("export_detail")
+        buf = C.create_string_buffer(need.value)
+        if self.L.ccka_host_export_detail(*args, buf, need.value, C.byref(need)) != 0:
+            self._err("export_detail")
+        return buf.value.decode()
 
     def export(self, world, results: dict, traj, fmt=EXPORT_PROMETHEUS, s0=0, n=None, first_id=0,
                start_unix_ms=0) -> str:

@@ -113,6 +113,11 @@ struct ccka_ctx {
   float* d_my = nullptr;
   int64_t mlp_n = 0, mlp_cap = 0;
   int last_engine = 0;       // 1 general, 2 single-deployment
+  // per-scenario summary breakdown (ccka_set_detail)
+  bool detail_on = false;
+  bool detail_valid = false;
+  DetailDev* d_detail = nullptr;
+  int64_t detail_count = 0;
 };
 
 static int fail(ccka_ctx* c, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
@@ -392,7 +397,7 @@ int32_t ccka_struct_sizes(int64_t* out, int32_t n) {
   const int64_t s[] = {sizeof(ccka_itype),    sizeof(ccka_pool),    sizeof(ccka_deployment),
                        sizeof(ccka_world),    sizeof(ccka_scenarios), sizeof(ccka_results),
                        sizeof(ccka_traj_rec), sizeof(ccka_totals),  sizeof(ccka_trace_gen),
-                       sizeof(ccka_grid_stats)};
+                       sizeof(ccka_grid_stats), sizeof(ccka_detail)};
   const int32_t m = (int32_t)(sizeof s / sizeof s[0]);
   int32_t k = 0;
   for (; k < m && k < n; ++k) out[k] = s[k];
@@ -437,8 +442,11 @@ static void free_results(ccka_ctx* c) {
   dfree(c->d_res);
   dfree(c->d_traj);
   dfree(c->d_parts);
+  dfree(c->d_detail);
   c->traj_count = 0;
   c->traj_valid = false;
+  c->detail_count = 0;
+  c->detail_valid = false;
 }
 
 void ccka_close(ccka_ctx* c) {
@@ -767,6 +775,17 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     }
     k.traj = c->d_traj;
   }
+  k.detail = nullptr;
+  if (c->detail_on) {
+    if (c->detail_count != c->N) {
+      dfree(c->d_detail);
+      if (hipMalloc((void**)&c->d_detail, (size_t)c->N * sizeof(DetailDev)) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "detail alloc");
+      c->detail_count = c->N;
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_detail, 0, (size_t)c->N * sizeof(DetailDev), c->stream));
+    k.detail = c->d_detail;
+  }
   k.N = c->N;
   k.NL = load_cols(c);
   k.trace_mod = c->n_traces;
@@ -780,7 +799,7 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
   k.maxn = w.max_nodes;
   for (int d = 0; d < CCKA_MAX_DEPLOY; ++d) k.prov[d] = c->prov[d];
   if (c->engine_mode == 0 && c->d1_world && !c->d1_ready && (rc = d1_prepare(c)) != CCKA_OK) return rc;
-  if (c->engine_mode == 0 && c->d1_world && c->d1_ok) {
+  if (c->engine_mode == 0 && c->d1_world && c->d1_ok && !c->detail_on) {
     // single-deployment engine: argmin tables for this rollout, then the rollout
     TableParams tp{};
     tp.price = c->d_price; tp.ci_gpwh = c->d_ci_gpwh; tp.types = c->d_types;
@@ -838,7 +857,25 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     c->last_engine = 1;
   }
   c->traj_valid = trajectory != 0;
+  c->detail_valid = c->detail_on;
   c->ran = true;
+  return CCKA_OK;
+}
+
+int ccka_set_detail(ccka_ctx* c, int32_t on) {
+  if (!c) return CCKA_EINVAL;
+  c->detail_on = on != 0;
+  return CCKA_OK;
+}
+
+int ccka_get_detail(ccka_ctx* c, ccka_detail* out, int64_t count) {
+  if (!c || !out) return CCKA_EINVAL;
+  if (!c->ran || !c->detail_valid) return fail(c, CCKA_ESTATE, "last rollout recorded no detail (ccka_set_detail)");
+  if (count != c->N) return fail(c, CCKA_EINVAL, "detail count %lld != %lld scenarios", (long long)count, (long long)c->N);
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpy2DAsync(out, sizeof(ccka_detail), c->d_detail, sizeof(DetailDev), sizeof(ccka_detail), (size_t)count,
+                             hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return CCKA_OK;
 }
 

@@ -7,6 +7,14 @@
 
 namespace ccka {
 
+// ccka_detail plus the per-group energy of the current clock hour (carbon is
+// charged per hour, SEMANTICS 3.H); zeroed before the launch
+struct DetailDev {
+  ccka_detail d;
+  int64_t e_hour[CCKA_MAX_POOLS];
+  int64_t base_e_hour;
+};
+
 struct KParams {
   const ccka_world* w;  // device copy (pools, deployments, scalars)
   const ccka_itype* types;
@@ -39,6 +47,7 @@ struct KParams {
   uint32_t* last_choice;
   uint32_t* hash;
   ccka_traj_rec* traj;  // nullable
+  DetailDev* detail;    // nullable: per-scenario summary breakdown (ccka_set_detail)
   int64_t N;
   int64_t NL;           // load columns: N, or the shared trace count
   int64_t trace_mod;    // 0: column = scenario; else column = (first_id + i) % trace_mod

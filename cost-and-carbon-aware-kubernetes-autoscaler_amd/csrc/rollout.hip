@@ -335,6 +335,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
   const bool active = i < p.N;
+  DetailDev* const det = active && p.detail ? p.detail + i : nullptr;
 
   Lds L;
   L.K = K;
@@ -534,6 +535,14 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         // carbon of the hour that just ended
         if (t > 0) gco2 += (double)e_hour * (ci_gpwmin * 1e-9);
         e_hour = 0;
+        if (det) {  // the same hourly charge per pool and for the base node group
+          for (int q = 0; q < NP; ++q) {
+            if (t > 0) det->d.pool_gco2[q] += (double)det->e_hour[q] * (ci_gpwmin * 1e-9);
+            det->e_hour[q] = 0;
+          }
+          if (t > 0) det->d.base_gco2 += (double)det->base_e_hour * (ci_gpwmin * 1e-9);
+          det->base_e_hour = 0;
+        }
         ci_gpwmin = s_ci[(rl * 24 + h) * 2 + 0];
         ci_gpwh = s_ci[(rl * 24 + h) * 2 + 1];
         base_price = (long long)base_nodes * tprice(L, rl, base_type, 0, 1);
@@ -896,6 +905,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             if (bc == 0) nsp++; else nod++;
             burn += price;
             launches++;
+            if (det) det->d.pool_launches[cpool]++;
             last_choice = choice;
             hash = (hash ^ choice) * 16777619u;
             step_last_type = bk;
@@ -1021,6 +1031,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           if (bc == 0) nsp++; else nod++;
           burn += bpr;
           launches++;
+          if (det) det->d.pool_launches[q]++;
           last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
           hash = (hash ^ last_choice) * 16777619u;
           step_last_type = bk;
@@ -1515,7 +1526,27 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           for (int d = 0; d < DMAX; ++d) if (d < D) use += (long long)npods[n][d] * upp[d];
           use = min(use, (long long)ty.alloc_cpu_m);
         }
-        e_step += ty.idle_nw + ty.dyn_nw_per_m * use;
+        const long long en = ty.idle_nw + ty.dyn_nw_per_m * use;
+        e_step += en;
+        if (det) {
+          const int q = ni_pool(ninfo[n]);
+          det->d.pool_cost_uphmin[q] += nprice[n];
+          det->d.pool_energy_nwmin[q] += en;
+          det->e_hour[q] += en;
+          if (ni_cap(ninfo[n]) == 0) det->d.pool_node_min_spot[q]++;
+          else det->d.pool_node_min_od[q]++;
+        }
+      }
+      if (det) {
+        det->d.base_cost_uphmin += base_price;
+        det->d.base_energy_nwmin += base_nw;
+        det->base_e_hour += base_nw;
+        for (int q = 0; q < NP; ++q) {
+          int cnt = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) cnt += ((used >> n) & 1u) && ni_pool(ninfo[n]) == q ? 1 : 0;
+          det->d.pool_peak_nodes[q] = max(det->d.pool_peak_nodes[q], cnt);
+        }
       }
       cost += burn + base_price;
       energy_nw += e_step;
@@ -1550,6 +1581,23 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   }
   if (!active) return;
   gco2 += (double)e_hour * (ci_gpwmin * 1e-9);
+  if (det) {
+    for (int q = 0; q < NP; ++q) {
+      det->d.pool_gco2[q] += (double)det->e_hour[q] * (ci_gpwmin * 1e-9);
+      int cnt = 0;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) cnt += ((used >> n) & 1u) && ni_pool(ninfo[n]) == q ? 1 : 0;
+      det->d.pool_final_nodes[q] = cnt;
+    }
+    det->d.base_gco2 += (double)det->base_e_hour * (ci_gpwmin * 1e-9);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      if (d < D) {
+        det->d.desired[d] = replicas[d];
+        det->d.ready[d] = rpods[d];
+        det->d.pending[d] = replicas[d] - rpods[d];
+      }
+  }
   int reps = 0;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) reps += d < D ? replicas[d] : 0;

@@ -4,7 +4,7 @@
 //       the exact payload demo_19 / demo_20 / demo_21 hand to `kubectl patch`
 //   ccka manifest <burst [--index I] | pdb | nodepools>
 //       the demo_30 Deployments / demo_10 PDB / our base NodePools (YAML)
-//   ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]...
+//   ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]... [--label KIND NAME LABELS]...
 //               [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]
 //               [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]
 //       ingest the manifests, build the world, roll one cluster forward on the
@@ -41,6 +41,7 @@ static int usage() {
                "       ccka patch <reset|offpeak|peak> --pool NAME [--json] [--fallback]\n"
                "       ccka manifest <burst [--index I] | pdb | nodepools>\n"
                "       ccka replay [--nodepools F] [--apply F]... [--patch KIND NAME TYPE FILE]...\n"
+               "                   [--label KIND NAME 'k=v ...']...\n"
                "                   [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]\n"
                "                   [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]\n"
                "                   [--drift] [--replace] [--kyverno]\n");
@@ -113,7 +114,7 @@ int main(int argc, char** argv) {
   std::string nodepools, catalog = "tiny", json_out, prom_out, csv_out;
   long long start_ms = 0;
   std::vector<std::string> applies;
-  std::vector<std::vector<std::string>> patches;
+  std::vector<std::vector<std::string>> patches, labels;
   int steps = 1440, max_nodes = 16, device = 0, drift = 0, replace = 0, kyverno = 0;
   long load_m = 100;
   for (int a = 2; a < argc; ++a) {
@@ -127,6 +128,10 @@ int main(int argc, char** argv) {
       std::vector<std::string> p;
       for (int k = 0; k < 4; ++k) p.push_back(next());
       patches.push_back(p);
+    } else if (!std::strcmp(argv[a], "--label")) {
+      std::vector<std::string> p;
+      for (int k = 0; k < 3; ++k) p.push_back(next());
+      labels.push_back(p);
     } else if (!std::strcmp(argv[a], "--catalog")) catalog = next();
     else if (!std::strcmp(argv[a], "--steps")) steps = std::atoi(next().c_str());
     else if (!std::strcmp(argv[a], "--max-nodes")) max_nodes = std::atoi(next().c_str());
@@ -166,7 +171,14 @@ int main(int argc, char** argv) {
     }
     ccka_host_burst_manifest(h, 0, buf, sizeof buf);
     if (ccka_host_apply(h, buf) != CCKA_OK) die_host(h, "pdb");
+    // demo_10_setup_configure.sh:61-62 (`kubectl label nodepool ... --overwrite || true`)
+    const char* sp = std::getenv("NP_SPOT");
+    const char* od = std::getenv("NP_OD");
+    (void)ccka_host_label(h, "NodePool", sp && *sp ? sp : "spot-preferred", "autoscale.strategy=cost carbon.simulated=low", 1);
+    (void)ccka_host_label(h, "NodePool", od && *od ? od : "on-demand-slo", "autoscale.strategy=slo carbon.simulated=medium", 1);
   }
+  for (auto& l : labels)  // kubectl label --overwrite
+    if (ccka_host_label(h, l[0].c_str(), l[1].c_str(), l[2].c_str(), 1) != CCKA_OK) die_host(h, "label");
   ccka_world w;
   if (ccka_host_build_world(h, catalog.c_str(), steps, max_nodes, &w) != CCKA_OK) die_host(h, "build world");
   // Karpenter drift on the zone switch / replacement consolidation (SEMANTICS 3.G0, 3.G2)
@@ -191,7 +203,10 @@ int main(int argc, char** argv) {
   chk(ccka_set_scenarios(ctx, &sc), "ccka_set_scenarios");
   std::vector<int32_t> load((size_t)steps * w.n_deploy, (int32_t)load_m);
   chk(ccka_set_load(ctx, load.data(), (int64_t)load.size()), "ccka_set_load");
+  chk(ccka_set_detail(ctx, 1), "ccka_set_detail");
   chk(ccka_rollout(ctx, 1), "ccka_rollout");
+  ccka_detail det;
+  chk(ccka_get_detail(ctx, &det, 1), "ccka_get_detail");
   int64_t cost, pend;
   double energy, gco2;
   int32_t slo, nsp, nod, lau, del, peak, frep, fnod;
@@ -200,7 +215,7 @@ int main(int argc, char** argv) {
   chk(ccka_get_results(ctx, &r), "ccka_get_results");
   std::vector<ccka_traj_rec> traj((size_t)steps);
   chk(ccka_get_trajectory(ctx, traj.data(), (int64_t)steps), "ccka_get_trajectory");
-  const int n = ccka_host_summary(h, &w, &r, traj.data(), buf, sizeof buf);
+  const int n = ccka_host_summary(h, &w, &r, traj.data(), &det, buf, sizeof buf);
   if (n < 0) die_host(h, "summary");
   std::fwrite(buf, 1, (size_t)n, stdout);
   if (!json_out.empty()) {
@@ -210,8 +225,34 @@ int main(int argc, char** argv) {
                  "{\"cost_uphmin\": %lld, \"energy_wmin\": %.17g, \"gco2\": %.17g, \"slo_minutes\": %d, "
                  "\"pending_pod_minutes\": %lld, \"node_min_spot\": %d, \"node_min_od\": %d, \"launches\": %d, "
                  "\"deletions\": %d, \"peak_nodes\": %d, \"final_replicas\": %d, \"final_nodes\": %d, "
-                 "\"last_choice\": %u, \"choice_hash\": %u}\n",
+                 "\"last_choice\": %u, \"choice_hash\": %u, \"detail\": {",
                  (long long)cost, energy, gco2, slo, (long long)pend, nsp, nod, lau, del, peak, frep, fnod, lc, hash);
+    auto arr64 = [&](const char* k, const int64_t* v, int m, bool last = false) {
+      std::fprintf(f, "\"%s\": [", k);
+      for (int i = 0; i < m; ++i) std::fprintf(f, "%s%lld", i ? ", " : "", (long long)v[i]);
+      std::fprintf(f, "]%s", last ? "" : ", ");
+    };
+    auto arr32 = [&](const char* k, const int32_t* v, int m) {
+      std::fprintf(f, "\"%s\": [", k);
+      for (int i = 0; i < m; ++i) std::fprintf(f, "%s%d", i ? ", " : "", v[i]);
+      std::fprintf(f, "], ");
+    };
+    const int P = w.n_pools, D = w.n_deploy;
+    arr64("pool_cost_uphmin", det.pool_cost_uphmin, P);
+    arr64("pool_energy_nwmin", det.pool_energy_nwmin, P);
+    std::fprintf(f, "\"pool_gco2\": [");
+    for (int i = 0; i < P; ++i) std::fprintf(f, "%s%.17g", i ? ", " : "", det.pool_gco2[i]);
+    std::fprintf(f, "], ");
+    arr32("pool_node_min_spot", det.pool_node_min_spot, P);
+    arr32("pool_node_min_od", det.pool_node_min_od, P);
+    arr32("pool_final_nodes", det.pool_final_nodes, P);
+    arr32("pool_peak_nodes", det.pool_peak_nodes, P);
+    arr32("pool_launches", det.pool_launches, P);
+    arr32("desired", det.desired, D);
+    arr32("ready", det.ready, D);
+    arr32("pending", det.pending, D);
+    std::fprintf(f, "\"base_cost_uphmin\": %lld, \"base_energy_nwmin\": %lld, \"base_gco2\": %.17g}}\n",
+                 (long long)det.base_cost_uphmin, (long long)det.base_energy_nwmin, det.base_gco2);
     std::fclose(f);
   }
   for (int fmt : {CCKA_EXPORT_PROMETHEUS, CCKA_EXPORT_CSV}) {
@@ -225,6 +266,13 @@ int main(int argc, char** argv) {
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) return 1;
     std::fputs(text.data(), f);
+    if (fmt == CCKA_EXPORT_PROMETHEUS) {  // the per-pool breakdown (carbon.simulated groups)
+      ccka_host_export_detail(h, &w, &det, 1, 0, start_ms, nullptr, 0, &need);
+      std::vector<char> t2((size_t)(need > 0 ? need : 1));
+      if (ccka_host_export_detail(h, &w, &det, 1, 0, start_ms, t2.data(), need, &need) != CCKA_OK)
+        die_host(h, "export detail");
+      std::fputs(t2.data(), f);
+    }
     std::fclose(f);
   }
   ccka_close(ctx);

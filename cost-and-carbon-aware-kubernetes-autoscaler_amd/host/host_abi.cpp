@@ -138,10 +138,52 @@ int ccka_host_build_world(ccka_host* h, const char* catalog, int32_t n_steps, in
   });
 }
 
-int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
-                      const ccka_traj_rec* traj, char* out, int64_t cap) {
+int ccka_host_label(ccka_host* h, const char* kind, const char* name, const char* labels, int32_t overwrite) {
+  return guarded(h, [&] {
+    if (!kind || !name || !labels) return (int)CCKA_EINVAL;
+    h->store.label(kind, name, labels, overwrite != 0);
+    return (int)CCKA_OK;
+  });
+}
+
+// NodePool disruption / requirements as configured at the run's last step:
+// the pool as created, the RESET profile (consolidateAfter per scenario 0),
+// then the peak or off-peak profile in force (merge semantics, SEMANTICS 3.A)
+static ccka_pool_patch pool_at_end(const ccka_world* w, int q, bool peak) {
+  ccka_pool_patch cur = w->pools[q].base;
+  ccka_pool_patch rp = w->pools[q].profile[CCKA_PROFILE_RESET];
+  if (rp.consolidate_after_s >= 0) rp.consolidate_after_s = w->reset_ca_s;
+  const ccka_pool_patch* steps[2] = {&rp, &w->pools[q].profile[peak ? CCKA_PROFILE_PEAK : CCKA_PROFILE_OFFPEAK]};
+  for (const ccka_pool_patch* x : steps) {
+    if (x->policy != CCKA_POLICY_KEEP) cur.policy = x->policy;
+    if (x->consolidate_after_s >= 0) cur.consolidate_after_s = x->consolidate_after_s;
+    if (x->zone_mask) cur.zone_mask = x->zone_mask;
+    if (x->cap_mask) cur.cap_mask = x->cap_mask;
+  }
+  return cur;
+}
+
+static bool peak_at(const ccka_world* w, int t) {
+  const int minute = (w->start_minute + t) % 1440, ps = w->peak_start_min, pe = w->peak_end_min;
+  const bool in = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
+  return w->peak_switch && in;
+}
+
+static std::string duration_text(int s) {
+  if (s % 3600 == 0 && s) return std::to_string(s / 3600) + "h";
+  if (s % 60 == 0 && s) return std::to_string(s / 60) + "m";
+  return std::to_string(s) + "s";
+}
+
+int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r, const ccka_traj_rec* traj,
+                      const ccka_detail* det, char* out, int64_t cap) {
   return guarded(h, [&] {
     if (!w || !r) return (int)CCKA_EINVAL;
+    const WorldMeta& M = h->meta;
+    auto pool_name = [&](int q) { return q < (int)M.pool_names.size() ? M.pool_names[(size_t)q] : std::string("?"); };
+    auto label_or = [](const std::vector<std::string>& v, int i, const char* dflt) {
+      return i < (int)v.size() && !v[(size_t)i].empty() ? v[(size_t)i] : std::string(dflt);
+    };
     std::string s;
     char b[512];
     const int T = w->n_steps;
@@ -149,29 +191,57 @@ int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
     std::snprintf(b, sizeof b, "horizon: %d steps x %d s   pools: %d   deployments: %d   catalog: %d types\n\n",
                   T, CCKA_STEP_SECONDS, w->n_pools, w->n_deploy, w->n_types);
     s += b;
-    s += "# NodePools (Karpenter order)\n";
+    // ---- NodePools: demo_20_offpeak_observe.sh:9-20 views at the last step
+    const bool peak = traj ? (traj[T - 1].flags & 1u) != 0 : peak_at(w, T - 1);
+    std::snprintf(b, sizeof b, "[Observe] Disruption settings (last step, %s profile)\n", peak ? "peak" : "off-peak");
+    s += b;
     for (int q = 0; q < w->n_pools; ++q) {
-      const char* nm = q < (int)h->meta.pool_names.size() ? h->meta.pool_names[(size_t)q].c_str() : "?";
-      std::snprintf(b, sizeof b, "  %-18s cap=%s%s zones=0x%x budget=%d%%\n", nm,
-                    (w->pools[q].base.cap_mask & CCKA_CAP_SPOT) ? "spot," : "",
-                    (w->pools[q].base.cap_mask & CCKA_CAP_OD) ? "on-demand" : "", w->pools[q].base.zone_mask,
+      const ccka_pool_patch e = pool_at_end(w, q, peak);
+      std::snprintf(b, sizeof b, "== %s ==\nconsolidationPolicy=%s  consolidateAfter=%s\n", pool_name(q).c_str(),
+                    e.policy == CCKA_WHEN_EMPTY ? "WhenEmpty" : "WhenEmptyOrUnderutilized",
+                    duration_text(e.consolidate_after_s).c_str());
+      s += b;
+      s += "topology.kubernetes.io/zone=In: ";
+      for (int z = 0; z < w->n_zones; ++z)
+        if (e.zone_mask >> z & 1u) s += M.zone_prefix + (char)('a' + z) + " ";
+      s += "\nkarpenter.sh/capacity-type=In: ";
+      if (e.cap_mask & CCKA_CAP_SPOT) s += "spot ";
+      if (e.cap_mask & CCKA_CAP_OD) s += "on-demand ";
+      std::snprintf(b, sizeof b, "\nlabels: autoscale.strategy=%s carbon.simulated=%s   budget: nodes %d%%",
+                    label_or(M.pool_strategy, q, "<none>").c_str(), label_or(M.pool_carbon, q, "<none>").c_str(),
                     w->pools[q].budget_pct);
       s += b;
+      if (w->pools[q].limit_cpu_m >= 0) {
+        std::snprintf(b, sizeof b, "   limits: cpu %dm", w->pools[q].limit_cpu_m);
+        s += b;
+      }
+      s += "\n";
     }
+    // ---- Deployments: demo_30_burst_observe.sh:10-11 custom columns
+    s += "\n# Summary of deployments (last step)\n";
+    std::snprintf(b, sizeof b, "%-24s %-7s %-8s %s\n", "NAME", "READY", "DESIRED", "CAPACITY");
+    s += b;
+    for (int d = 0; d < w->n_deploy; ++d) {
+      if (w->deploy[d].scaler == CCKA_SCALER_KEDA_TRIGGER) continue;  // a trigger, not a Deployment
+      const std::string nm = d < (int)M.deploy_names.size() ? M.deploy_names[(size_t)d] : "?";
+      // kubectl omits status.readyReplicas at 0 -> "<none>"
+      std::string ready = "<none>", desired = std::to_string(w->deploy[d].replicas0) + "*";
+      if (det) {
+        if (det->ready[d] > 0) ready = std::to_string(det->ready[d]);
+        desired = std::to_string(det->desired[d]);
+      }
+      std::snprintf(b, sizeof b, "%-24s %-7s %-8s %s\n", nm.c_str(), ready.c_str(), desired.c_str(),
+                    label_or(M.deploy_capacity, d, "<none>").c_str());
+      s += b;
+    }
+    if (!det) s += "(* manifest replicas: run with the detail breakdown for the rollout's values)\n";
     if (traj) {
       const ccka_traj_rec& last = traj[T - 1];
-      std::snprintf(b, sizeof b, "\n# Final step: replicas=%d pending=%d nodes spot=%u on-demand=%u\n",
-                    last.replicas, last.pending, last.nodes_spot, last.nodes_od);
+      std::snprintf(b, sizeof b, "pods: desired=%d pending=%d   nodes: spot=%u on-demand=%u\n", last.replicas,
+                    last.pending, last.nodes_spot, last.nodes_od);
       s += b;
     }
-    s += "\n# Deployments (NAME DESIRED CAPACITY)\n";
-    for (int d = 0; d < w->n_deploy; ++d) {
-      const char* nm = d < (int)h->meta.deploy_names.size() ? h->meta.deploy_names[(size_t)d].c_str() : "?";
-      const uint32_t c = w->deploy[d].cap_sel;
-      std::snprintf(b, sizeof b, "  %-18s %-5d %s\n", nm, w->deploy[d].replicas0,
-                    c == CCKA_CAP_SPOT ? "spot" : c == CCKA_CAP_OD ? "on-demand" : "any");
-      s += b;
-    }
+    // ---- nodes
     const uint32_t lc = r->last_choice ? r->last_choice[0] : 0xFFFFFFFFu;
     s += "\n# Nodes\n";
     std::snprintf(b, sizeof b, "  node-minutes spot=%d on-demand=%d   peak nodes=%d   launches=%d deletions=%d\n",
@@ -179,13 +249,53 @@ int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
     s += b;
     if (lc != 0xFFFFFFFFu) {
       const int k = (int)(lc & 0xFFF), z = (int)((lc >> 12) & 3), c = (int)((lc >> 14) & 3), q = (int)(lc >> 16);
-      std::snprintf(b, sizeof b, "  last launch: %s zone=%c capacity=%s pool=%s\n",
-                    k < (int)h->tables.names.size() ? h->tables.names[(size_t)k].c_str() : "?", 'a' + z,
-                    c == 0 ? "spot" : "on-demand",
-                    q < (int)h->meta.pool_names.size() ? h->meta.pool_names[(size_t)q].c_str() : "?");
+      std::snprintf(b, sizeof b, "  last launch: %s zone=%s%c capacity=%s pool=%s\n",
+                    k < (int)h->tables.names.size() ? h->tables.names[(size_t)k].c_str() : "?", M.zone_prefix.c_str(),
+                    'a' + z, c == 0 ? "spot" : "on-demand", pool_name(q).c_str());
       s += b;
     }
-    s += "\n# Cost and carbon\n";
+    // ---- cost and carbon by pool and by carbon.simulated group
+    if (det) {
+      s += "\n# Cost and carbon by node pool\n";
+      std::snprintf(b, sizeof b, "%-24s %-8s %10s %10s %15s %8s %11s %12s %12s\n", "NODEPOOL", "CARBON", "NODEMIN-S",
+                    "NODEMIN-OD", "NODES(END/PEAK)", "LAUNCHES", "COST($)", "ENERGY(kWh)", "gCO2");
+      s += b;
+      std::vector<std::pair<std::string, double>> gcost, gkwh, gco2;
+      auto add = [](std::vector<std::pair<std::string, double>>& v, const std::string& k, double x) {
+        for (auto& e : v)
+          if (e.first == k) { e.second += x; return; }
+        v.push_back({k, x});
+      };
+      for (int q = 0; q < w->n_pools; ++q) {
+        const std::string grp = label_or(M.pool_carbon, q, "<none>");
+        const double usd = (double)det->pool_cost_uphmin[q] / 6e7, kwh = (double)det->pool_energy_nwmin[q] * 1e-9 / 6e4;
+        std::snprintf(b, sizeof b, "%-24s %-8s %10d %10d %15s %8d %11.4f %12.4f %12.2f\n", pool_name(q).c_str(),
+                      grp.c_str(), det->pool_node_min_spot[q], det->pool_node_min_od[q],
+                      (std::to_string(det->pool_final_nodes[q]) + "/" + std::to_string(det->pool_peak_nodes[q])).c_str(),
+                      det->pool_launches[q], usd, kwh, det->pool_gco2[q]);
+        s += b;
+        add(gcost, grp, usd);
+        add(gkwh, grp, kwh);
+        add(gco2, grp, det->pool_gco2[q]);
+      }
+      const double busd = (double)det->base_cost_uphmin / 6e7, bkwh = (double)det->base_energy_nwmin * 1e-9 / 6e4;
+      std::snprintf(b, sizeof b, "%-24s %-8s %10s %10d %15s %8s %11.4f %12.4f %12.2f\n", "(base managed nodes)", "<none>",
+                    "-", w->base_nodes * T, (std::to_string(w->base_nodes) + "/" + std::to_string(w->base_nodes)).c_str(),
+                    "-", busd, bkwh, det->base_gco2);
+      s += b;
+      add(gcost, "<none>", busd);
+      add(gkwh, "<none>", bkwh);
+      add(gco2, "<none>", det->base_gco2);
+      s += "\n# By carbon.simulated group (demo_10_setup_configure.sh:61-62 labels)\n";
+      std::snprintf(b, sizeof b, "%-10s %11s %12s %12s\n", "GROUP", "COST($)", "ENERGY(kWh)", "gCO2");
+      s += b;
+      for (size_t g = 0; g < gcost.size(); ++g) {
+        std::snprintf(b, sizeof b, "%-10s %11.4f %12.4f %12.2f\n", gcost[g].first.c_str(), gcost[g].second,
+                      gkwh[g].second, gco2[g].second);
+        s += b;
+      }
+    }
+    s += "\n# Cost and carbon (run total)\n";
     std::snprintf(b, sizeof b, "  cost=$%.4f   energy=%.4f kWh   carbon=%.2f gCO2\n", (double)r->cost_uphmin[0] / 6e7,
                   r->energy_wmin[0] / 6e4, r->gco2[0]);
     s += b;
@@ -329,6 +439,78 @@ int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const cc
         }
       }
     }
+    if (needed) *needed = (int64_t)o.size() + 1;
+    if (!out || (int64_t)o.size() + 1 > cap) {
+      h->err = "output buffer too small: need " + std::to_string(o.size() + 1);
+      return (int)CCKA_EINVAL;
+    }
+    std::memcpy(out, o.data(), o.size());
+    out[o.size()] = 0;
+    return (int)CCKA_OK;
+  });
+}
+
+int ccka_host_export_detail(ccka_host* h, const ccka_world* w, const ccka_detail* det, int64_t n, int64_t first_id,
+                            int64_t start_unix_ms, char* out, int64_t cap, int64_t* needed) {
+  return guarded(h, [&] {
+    if (needed) *needed = 0;
+    if (!w || !det || n < 0 || w->n_steps < 1) return (int)CCKA_EINVAL;
+    const WorldMeta& M = h->meta;
+    const long long ts = (long long)(start_unix_ms + (int64_t)(w->n_steps - 1) * CCKA_STEP_SECONDS * 1000);
+    std::string o;
+    char b[640];
+    auto family = [&](const char* name, const char* type, const char* help) {
+      std::snprintf(b, sizeof b, "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
+      o += b;
+    };
+    auto lab = [&](const std::vector<std::string>& v, int q) { return q < (int)v.size() ? v[(size_t)q] : std::string(); };
+    // one sample per (scenario, group); group P = the base managed node group
+    auto pool_series = [&](const char* name, const char* type, const char* help, auto value) {
+      family(name, type, help);
+      for (int64_t s = 0; s < n; ++s)
+        for (int q = 0; q <= w->n_pools; ++q) {
+          const bool base = q == w->n_pools;
+          const std::string np = base ? std::string("base-managed") : (q < (int)M.pool_names.size() ? M.pool_names[(size_t)q] : "?");
+          std::snprintf(b, sizeof b,
+                        "%s{scenario=\"%lld\",nodepool=\"%s\",carbon_simulated=\"%s\",autoscale_strategy=\"%s\"} %.17g %lld\n",
+                        name, (long long)(first_id + s), np.c_str(), base ? "" : lab(M.pool_carbon, q).c_str(),
+                        base ? "" : lab(M.pool_strategy, q).c_str(), value(det[s], q, base), ts);
+          o += b;
+        }
+    };
+    pool_series("ccka_nodepool_cost_dollars_total", "counter", "Node cost of the run per NodePool (base: managed node group).",
+                [](const ccka_detail& d, int q, bool base) { return (double)(base ? d.base_cost_uphmin : d.pool_cost_uphmin[q]) / 6e7; });
+    pool_series("ccka_nodepool_energy_kwh_total", "counter", "Node energy of the run per NodePool.",
+                [](const ccka_detail& d, int q, bool base) {
+                  return (double)(base ? d.base_energy_nwmin : d.pool_energy_nwmin[q]) * 1e-9 / 6e4;
+                });
+    pool_series("ccka_nodepool_carbon_grams_total", "counter", "Operational carbon of the run per NodePool.",
+                [](const ccka_detail& d, int q, bool base) { return base ? d.base_gco2 : d.pool_gco2[q]; });
+    pool_series("ccka_nodepool_nodes", "gauge", "Nodes of the NodePool at the last step.",
+                [&](const ccka_detail& d, int q, bool base) { return (double)(base ? w->base_nodes : d.pool_final_nodes[q]); });
+    pool_series("ccka_nodepool_launches_total", "counter", "NodeClaims launched per NodePool.",
+                [](const ccka_detail& d, int q, bool base) { return base ? 0.0 : (double)d.pool_launches[q]; });
+    family("ccka_nodepool_node_minutes_total", "counter", "Karpenter node-minutes per NodePool and capacity type.");
+    for (int64_t s = 0; s < n; ++s)
+      for (int q = 0; q < w->n_pools; ++q)
+        for (int c = 0; c < 2; ++c) {
+          std::snprintf(b, sizeof b,
+                        "ccka_nodepool_node_minutes_total{scenario=\"%lld\",nodepool=\"%s\",carbon_simulated=\"%s\","
+                        "capacity_type=\"%s\"} %d %lld\n",
+                        (long long)(first_id + s), q < (int)M.pool_names.size() ? M.pool_names[(size_t)q].c_str() : "?",
+                        lab(M.pool_carbon, q).c_str(), c == 0 ? "spot" : "on-demand",
+                        c == 0 ? det[s].pool_node_min_spot[q] : det[s].pool_node_min_od[q], ts);
+          o += b;
+        }
+    family("kube_deployment_status_replicas_ready", "gauge", "The number of ready replicas per deployment (last step).");
+    for (int64_t s = 0; s < n; ++s)
+      for (int d = 0; d < w->n_deploy; ++d) {
+        if (w->deploy[d].scaler == CCKA_SCALER_KEDA_TRIGGER) continue;
+        std::snprintf(b, sizeof b, "kube_deployment_status_replicas_ready{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %d %lld\n",
+                      h->env.ns.c_str(), d < (int)M.deploy_names.size() ? M.deploy_names[(size_t)d].c_str() : "?",
+                      (long long)(first_id + s), det[s].ready[d], ts);
+        o += b;
+      }
     if (needed) *needed = (int64_t)o.size() + 1;
     if (!out || (int64_t)o.size() + 1 > cap) {
       h->err = "output buffer too small: need " + std::to_string(o.size() + 1);

@@ -65,6 +65,43 @@ void ManifestStore::patch(const std::string& kind, const std::string& name, cons
   *o = std::move(copy);
 }
 
+void ManifestStore::label(const std::string& kind, const std::string& name, const std::string& labels,
+                          bool overwrite) {
+  Value* o = find(kind, name);
+  if (!o) throw ParseError("Error from server (NotFound): " + kind + " \"" + name + "\" not found");
+  Value copy = *o;
+  Value* md = copy.get("metadata");
+  if (!md || !md->is_map()) throw ParseError("label: object without metadata");
+  Value* ls = md->get("labels");
+  if (!ls) ls = &md->set("labels", Value::object());
+  if (!ls->is_map()) throw ParseError("label: metadata.labels is not a map");
+  size_t i = 0;
+  int n = 0;
+  while (i < labels.size()) {
+    while (i < labels.size() && std::isspace((unsigned char)labels[i])) ++i;
+    size_t j = i;
+    while (j < labels.size() && !std::isspace((unsigned char)labels[j])) ++j;
+    if (j == i) break;
+    const std::string tok = labels.substr(i, j - i);
+    i = j;
+    ++n;
+    const size_t eq = tok.find('=');
+    if (eq == std::string::npos) {
+      if (tok.size() < 2 || tok.back() != '-') throw ParseError("error: at least one label update is required");
+      ls->erase(tok.substr(0, tok.size() - 1));
+      continue;
+    }
+    const std::string key = tok.substr(0, eq), val = tok.substr(eq + 1);
+    if (key.empty()) throw ParseError("error: invalid label spec: " + tok);
+    if (const Value* cur = ls->get(key); cur && cur->as_string() != val && !overwrite)
+      throw ParseError("error: '" + key + "' already has a value (" + cur->as_string() +
+                       "), and --overwrite is false");
+    ls->set(key, Value::str(val));
+  }
+  if (!n) throw ParseError("error: at least one label update is required");
+  *o = std::move(copy);
+}
+
 // ------------------------------------------------------------------ tables
 int Tables::index(const std::string& n) const {
   for (size_t k = 0; k < names.size(); ++k)
@@ -161,6 +198,8 @@ static int policy_code(const std::string& s) {
   throw ParseError("unknown consolidationPolicy " + s);
 }
 
+static thread_local std::string g_zone_prefix_seen;  // region prefix of the last zone name parsed (summary names)
+
 static void requirements_masks(const Value* reqs, uint32_t* zm, uint32_t* cm) {
   if (!reqs || !reqs->is_seq()) return;
   for (auto& r : reqs->seq) {
@@ -171,7 +210,10 @@ static void requirements_masks(const Value* reqs, uint32_t* zm, uint32_t* cm) {
     uint32_t m = 0;
     for (auto& v : vals->seq) {
       const std::string s = v.as_string();
-      if (key == "topology.kubernetes.io/zone") m |= zone_bit(s);
+      if (key == "topology.kubernetes.io/zone") {
+        m |= zone_bit(s);
+        if (!s.empty()) g_zone_prefix_seen = s.substr(0, s.size() - 1);
+      }
       else if (key == "karpenter.sh/capacity-type") m |= s == "spot" ? CCKA_CAP_SPOT : s == "on-demand" ? CCKA_CAP_OD : 0;
     }
     if (key == "topology.kubernetes.io/zone") *zm = m;
@@ -239,6 +281,7 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
                       int max_nodes, ccka_world* w) {
   std::memset(w, 0, sizeof *w);
   WorldMeta meta;
+  g_zone_prefix_seen.clear();
   // ---- NodePools, Karpenter order: weight desc, name asc
   auto pools = store.all("NodePool");
   if (pools.empty()) throw ParseError("no NodePool objects");
@@ -255,6 +298,10 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
     const Value& np = *pools[q];
     const std::string name = name_of(np);
     meta.pool_names.push_back(name);
+    const Value* cl = np.at({"metadata", "labels", "carbon.simulated"});
+    const Value* sl = np.at({"metadata", "labels", "autoscale.strategy"});
+    meta.pool_carbon.push_back(cl ? cl->as_string() : "");
+    meta.pool_strategy.push_back(sl ? sl->as_string() : "");
     ccka_pool& P = w->pools[q];
     P.limit_cpu_m = -1;
     if (const Value* l = np.at({"spec", "limits", "cpu"})) P.limit_cpu_m = (int32_t)cpu_millis(l->as_string());
@@ -304,6 +351,8 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
     const Value& dv = *deps[d];
     const std::string name = name_of(dv);
     meta.deploy_names.push_back(name);
+    const Value* capl = dv.at({"metadata", "labels", "capacity"});
+    meta.deploy_capacity.push_back(capl ? capl->as_string() : "");
     ccka_deployment& D = w->deploy[d];
     D.scaler = CCKA_SCALER_STATIC;
     D.replicas0 = (int32_t)(dv.at({"spec", "replicas"}) ? dv.at({"spec", "replicas"})->as_int() : 1);
@@ -378,10 +427,11 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
   if (n_extra) {
     if (deps.size() + n_extra > CCKA_MAX_DEPLOY) throw ParseError("more than 16 Deployments + extra KEDA triggers");
     std::vector<ccka_deployment> out;
-    std::vector<std::string> names;
+    std::vector<std::string> names, caps;
     for (size_t d = 0; d < deps.size(); ++d) {
       out.push_back(w->deploy[d]);
       names.push_back(meta.deploy_names[d]);
+      caps.push_back(meta.deploy_capacity[d]);
       for (size_t j = 0; j < extra[d].size(); ++j) {
         ccka_deployment T{};
         T.scaler = CCKA_SCALER_KEDA_TRIGGER;
@@ -393,12 +443,15 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
         T.down = rules_from(nullptr, false, 300);
         out.push_back(T);
         names.push_back(meta.deploy_names[d] + "/trigger-" + std::to_string(j + 1));
+        caps.push_back(meta.deploy_capacity[d]);
       }
     }
     for (size_t d = 0; d < out.size(); ++d) w->deploy[d] = out[d];
     w->n_deploy = (int32_t)out.size();
     meta.deploy_names = names;
+    meta.deploy_capacity = caps;
   }
+  if (!g_zone_prefix_seen.empty()) meta.zone_prefix = g_zone_prefix_seen;
   // ---- catalog, tiles, cluster defaults
   w->n_steps = n_steps;
   w->start_minute = 0;

@@ -28,6 +28,10 @@ class ManifestStore {
   // kubectl patch <kind> <name> --type=merge|json; throws ParseError
   void patch(const std::string& kind, const std::string& name, const std::string& type,
              const std::string& patch_text);
+  // kubectl label <kind> <name> k=v... [--overwrite] (demo_10_setup_configure.sh:61-62):
+  // whitespace-separated "k=v" set, "k-" removes; an existing different value
+  // without overwrite fails like kubectl; throws ParseError
+  void label(const std::string& kind, const std::string& name, const std::string& labels, bool overwrite);
   const Value* get(const std::string& kind, const std::string& name) const;
   std::vector<const Value*> all(const std::string& kind) const;
 
@@ -52,6 +56,12 @@ Tables builtin_tables(const std::string& which, double ci_g_per_kwh = 400.0, uin
 struct WorldMeta {
   std::vector<std::string> pool_names;    // Karpenter order
   std::vector<std::string> deploy_names;  // engine deployment index order
+  // NodePool labels the reference sets for grouping in OpenCost / dashboards
+  // (demo_10_setup_configure.sh:61-62), "" when absent
+  std::vector<std::string> pool_carbon;    // carbon.simulated
+  std::vector<std::string> pool_strategy;  // autoscale.strategy
+  std::vector<std::string> deploy_capacity;  // Deployment label `capacity` (demo_30 :88)
+  std::string zone_prefix = "us-east-2";     // zone bit z = zone_prefix + 'a' + z
 };
 
 // The reference's base NodePools (it never creates them, demo_00_env.sh:17):

@@ -63,6 +63,8 @@ static int run_world(ccka_host* h) {
     if (ccka_host_apply(h, buf.data()) != CCKA_OK) return 2;
   }
   ccka_world w;
+  (void)ccka_host_label(h, "NodePool", "spot-preferred", "autoscale.strategy=cost carbon.simulated=low", 1);
+  (void)ccka_host_label(h, "NodePool", "on-demand-slo", "carbon.simulated=medium x=y x- bad", 0);
   if (ccka_host_build_world(h, "tiny", 360, 16, &w) != CCKA_OK) return 3;
   w.disrupt_ext = CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE;
   const int64_t n = 3, T = w.n_steps, D = w.n_deploy;
@@ -82,15 +84,20 @@ static int run_world(ccka_host* h) {
   ccka_results r{cost.data(), en.data(), co2.data(), i32[0].data(), ppm.data(), i32[1].data(), i32[2].data(),
                  i32[3].data(), i32[4].data(), i32[5].data(), i32[6].data(), i32[7].data(), lc.data(), hs.data()};
   std::vector<ccka_traj_rec> traj((size_t)(T * n));
-  if (ccka_oracle_rollout(&w, &sc, load.data(), &r, traj.data(), 2) != CCKA_OK) return 4;
+  std::vector<ccka_detail> det((size_t)n);
+  if (ccka_oracle_rollout_detail(&w, &sc, load.data(), &r, traj.data(), det.data(), 2) != CCKA_OK) return 4;
   ccka_totals tot;
   ccka_oracle_totals(&r, n, &tot);
-  if (ccka_host_summary(h, &w, &r, traj.data(), buf.data(), (int64_t)buf.size()) < 0) return 5;
+  if (ccka_host_summary(h, &w, &r, traj.data(), det.data(), buf.data(), (int64_t)buf.size()) < 0) return 5;
+  if (ccka_host_summary(h, &w, &r, nullptr, nullptr, buf.data(), (int64_t)buf.size()) < 0) return 5;
   int64_t need = 0;
   for (int f : {CCKA_EXPORT_PROMETHEUS, CCKA_EXPORT_CSV})
     if (ccka_host_export(h, f, &w, traj.data(), n, &r, 0, n, 0, 1700000000000LL, buf.data(), (int64_t)buf.size(),
                          &need) != CCKA_OK)
       return 6;
+  if (ccka_host_export_detail(h, &w, det.data(), n, 0, 1700000000000LL, buf.data(), (int64_t)buf.size(), &need) !=
+      CCKA_OK)
+    return 7;
   std::printf("world ok: %lld scenarios x %lld steps, launches %lld deletions %lld\n", (long long)n, (long long)T,
               (long long)tot.launches, (long long)tot.deletions);
   return 0;

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CCKA_ABI_VERSION 2
+#define CCKA_ABI_VERSION 3
 
 #define CCKA_STEP_SECONDS 60
 #define CCKA_MAX_TYPES 1024
@@ -208,6 +208,31 @@ typedef struct ccka_results {
   uint32_t* choice_hash;
 } ccka_results;
 
+/* Per-scenario breakdown behind the demo_41 summary (ccka_set_detail): the
+ * run's cost / energy / carbon / node-minutes per NodePool and for the base
+ * managed node group (01_cluster.sh:24-30), and per Deployment the final
+ * DESIRED (spec.replicas after the scaler) / READY (pods on ready nodes,
+ * status.readyReplicas) / pending, the columns of demo_30_burst_observe.sh:10-11.
+ * Pool p's sums cover the Karpenter nodes of that pool; totals = base + pools
+ * (exact for the integer fields; gCO2 is charged per clock hour per group, as
+ * the run total is, SEMANTICS 3.H). 392 bytes. */
+typedef struct ccka_detail {
+  int64_t pool_cost_uphmin[CCKA_MAX_POOLS];
+  int64_t pool_energy_nwmin[CCKA_MAX_POOLS];  /* nanowatt-minutes, exact */
+  double pool_gco2[CCKA_MAX_POOLS];
+  int32_t pool_node_min_spot[CCKA_MAX_POOLS];
+  int32_t pool_node_min_od[CCKA_MAX_POOLS];
+  int32_t pool_final_nodes[CCKA_MAX_POOLS];
+  int32_t pool_peak_nodes[CCKA_MAX_POOLS];
+  int32_t pool_launches[CCKA_MAX_POOLS];
+  int32_t desired[CCKA_MAX_DEPLOY];
+  int32_t ready[CCKA_MAX_DEPLOY];
+  int32_t pending[CCKA_MAX_DEPLOY];
+  int64_t base_cost_uphmin;
+  int64_t base_energy_nwmin;
+  double base_gco2;
+} ccka_detail;
+
 /* Trajectory record, one per (step, scenario), layout [T][N]. 16 bytes. */
 typedef struct ccka_traj_rec {
   int32_t replicas;
@@ -261,7 +286,7 @@ typedef struct ccka_ctx ccka_ctx;
 int32_t ccka_abi_version(void);
 /* sizes of the ABI structs, for binding self-checks: fills out[0..n) in the
  * order itype, pool, deployment, world, scenarios, results, traj_rec, totals,
- * trace_gen; returns the count written. */
+ * trace_gen, grid_stats, detail; returns the count written. */
 int32_t ccka_struct_sizes(int64_t* out, int32_t n);
 int ccka_open(ccka_ctx** out, int device_ordinal);
 void ccka_close(ccka_ctx* ctx);
@@ -292,6 +317,12 @@ int ccka_last_kernel_ms(ccka_ctx* ctx, double* ms);
 int ccka_get_results(ccka_ctx* ctx, ccka_results* out);
 int ccka_get_trajectory(ccka_ctx* ctx, ccka_traj_rec* out, int64_t count);
 int ccka_get_totals(ccka_ctx* ctx, ccka_totals* out);
+/* on != 0: later rollouts also record the per-scenario ccka_detail (the
+ * summary path: the run takes the general kernel; results are unchanged). */
+int ccka_set_detail(ccka_ctx* ctx, int32_t on);
+/* Copy the last rollout's details [count == n scenarios]; CCKA_ESTATE when it
+ * ran without ccka_set_detail. */
+int ccka_get_detail(ccka_ctx* ctx, ccka_detail* out, int64_t count);
 
 /* ---- policy sweep (BASELINE config 4) -------------------------------- */
 /* Per-grid sums of the last rollout's results. The batch must hold whole

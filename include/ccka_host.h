@@ -15,6 +15,7 @@
  *                           demo_19 :68-75), byte-identical to what the scripts send
  *   ccka_host_burst_manifest demo_30_burst_configure.sh:78-141 heredoc, byte-identical
  *   ccka_host_build_world   the stored objects -> ccka_world for libccka (ccka.h)
+ *   ccka_host_label         `kubectl label nodepool ... --overwrite` (demo_10_setup_configure.sh:61-62)
  *   ccka_host_summary       the missing demo_41_observe_cost_nodes.sh (README.md:57)
  * Environment names follow the scripts: NP_SPOT, NP_OD, OFFPEAK_ZONES,
  * PEAK_ZONES, NAMESPACE, COUNT, REPLICAS (demo_00_env.sh, demo_30 :7-8),
@@ -68,10 +69,23 @@ int ccka_host_burst_manifest(ccka_host* h, int32_t index, char* out, int64_t cap
  * stay valid until the next build or ccka_host_close. */
 int ccka_host_build_world(ccka_host* h, const char* catalog, int32_t n_steps, int32_t max_nodes,
                           ccka_world* out);
-/* demo_41-style summary of scenario 0 (results arrays of length >= 1;
- * traj may be NULL) */
+/* kubectl label <kind> <name> <labels> [--overwrite]: labels is a
+ * whitespace-separated list of "key=value" (set) and "key-" (remove); a key
+ * that already holds a different value fails unless overwrite (kubectl's
+ * message). The reference labels its NodePools carbon.simulated=low|medium and
+ * autoscale.strategy=cost|slo "for grouping in OpenCost/dashboards"; the world
+ * builder carries them as each pool's group in the summary and export. */
+int ccka_host_label(ccka_host* h, const char* kind, const char* name, const char* labels, int32_t overwrite);
+
+/* demo_41-style summary of scenario 0 (results arrays of length >= 1; traj and
+ * detail may be NULL). Sections: the NodePools' disruption settings and
+ * requirements at the last step (demo_20_offpeak_observe.sh:9-20 views) with
+ * their labels; the Deployments as NAME READY DESIRED CAPACITY
+ * (demo_30_burst_observe.sh:10-11 custom columns); nodes; with detail, cost /
+ * energy / gCO2 / node-minutes per NodePool and the base node group, and per
+ * carbon.simulated group; run totals. */
 int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r,
-                      const ccka_traj_rec* traj, char* out, int64_t cap);
+                      const ccka_traj_rec* traj, const ccka_detail* detail, char* out, int64_t cap);
 
 /* Trajectory export, the downstream wire format of the reference's observe
  * path (kube-state-metrics scraped into Prometheus/AMP for Grafana and
@@ -93,6 +107,14 @@ enum { CCKA_EXPORT_PROMETHEUS = 1, CCKA_EXPORT_CSV = 2 };
 int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const ccka_traj_rec* traj,
                      int64_t traj_n, const ccka_results* r, int64_t s0, int64_t n, int64_t first_id,
                      int64_t start_unix_ms, char* out, int64_t cap, int64_t* needed);
+/* Prometheus text of the per-pool breakdown of detail[0..n) at the last
+ * step: ccka_nodepool_{cost_dollars,energy_kwh,carbon_grams,launches}_total,
+ * ccka_nodepool_nodes, ccka_nodepool_node_minutes_total{capacity_type}, each
+ * labelled nodepool / carbon_simulated / autoscale_strategy (the base managed
+ * node group as nodepool="base-managed"), and
+ * kube_deployment_status_replicas_ready. Buffer rules as ccka_host_export. */
+int ccka_host_export_detail(ccka_host* h, const ccka_world* w, const ccka_detail* detail, int64_t n,
+                            int64_t first_id, int64_t start_unix_ms, char* out, int64_t cap, int64_t* needed);
 
 #ifdef __cplusplus
 }

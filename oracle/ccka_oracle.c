@@ -323,6 +323,7 @@ typedef struct {
   double gco2;
   int slo, nmin_spot, nmin_od, launches, deletions, peak_nodes;
   uint32_t last_choice, hash;
+  int pool_launches[CCKA_MAX_POOLS];
 } o_state;
 
 /* Karpenter drift: the node's zone or capacity type no longer satisfies its
@@ -407,6 +408,7 @@ static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, 
   nd->last_event = t;
   nd->src1 = src + 1;
   st->launches++;
+  st->pool_launches[p]++;
   st->last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)p << 16;
   st->hash = (st->hash ^ st->last_choice) * 16777619u;
 }
@@ -427,8 +429,10 @@ static int o_drifted(const o_state* st, const o_node* nd) {
   return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
 }
 
+/* det (optional): the per-pool / base-group / per-deployment breakdown of
+ * ccka_detail, accounted exactly as the run totals (SEMANTICS 3.H) */
 static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* load, int64_t i,
-                      int64_t nsc, ccka_results* out, ccka_traj_rec* traj) {
+                      int64_t nsc, ccka_results* out, ccka_traj_rec* traj, ccka_detail* det) {
   const ccka_world* w = e->w;
   const int D = e->D, NN = e->N;
   o_state st;
@@ -473,6 +477,8 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
                           (bt->idle_nw + bt->dyn_nw_per_m * (int64_t)(w->base_util * (double)bt->alloc_cpu_m));
   int prev_h = -1;
   const int ps = w->peak_start_min, pe = w->peak_end_min;
+  int64_t pool_eh[CCKA_MAX_POOLS] = {0}, base_eh = 0; /* detail: energy of the current clock hour */
+  if (det) memset(det, 0, sizeof *det);
 
   for (int t = 0; t < w->n_steps; ++t) {
     const int minute = (w->start_minute + t) % 1440;
@@ -481,6 +487,14 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     if (prev_h >= 0 && h != prev_h) {
       st.gco2 += (double)st.e_hour * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
       st.e_hour = 0;
+      if (det) {
+        for (int p = 0; p < w->n_pools; ++p) {
+          det->pool_gco2[p] += (double)pool_eh[p] * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
+          pool_eh[p] = 0;
+        }
+        det->base_gco2 += (double)base_eh * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
+        base_eh = 0;
+      }
     }
     prev_h = h;
     uint16_t flags = 0;
@@ -700,6 +714,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
         for (int d = 0; d < D; ++d) nd->pods[d] = cl->pods[d];
         pool_use[cl->pool] += (int64_t)w->types[bk].vcpu * 1000;
         st.launches++;
+        st.pool_launches[cl->pool]++;
         st.last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)cl->pool << 16;
         st.hash = (st.hash ^ st.last_choice) * 16777619u;
         step_last_type = (uint16_t)bk;
@@ -945,6 +960,22 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
         }
         e_step += ty->idle_nw + ty->dyn_nw_per_m * use;
         if (nd->cap == 0) nsp++; else nod++;
+        if (det) {
+          det->pool_cost_uphmin[nd->pool] += o_price(e, r, h, nd->type, nd->zone, nd->cap);
+          det->pool_energy_nwmin[nd->pool] += ty->idle_nw + ty->dyn_nw_per_m * use;
+          pool_eh[nd->pool] += ty->idle_nw + ty->dyn_nw_per_m * use;
+          if (nd->cap == 0) det->pool_node_min_spot[nd->pool]++; else det->pool_node_min_od[nd->pool]++;
+        }
+      }
+      if (det) {
+        det->base_cost_uphmin += (int64_t)w->base_nodes * o_price(e, r, h, w->base_type, 0, 1);
+        det->base_energy_nwmin += base_nw;
+        base_eh += base_nw;
+        for (int p = 0; p < w->n_pools; ++p) {
+          int cnt = 0;
+          for (int n = 0; n < NN; ++n) cnt += st.nodes[n].used && st.nodes[n].pool == p;
+          if (cnt > det->pool_peak_nodes[p]) det->pool_peak_nodes[p] = cnt;
+        }
       }
       st.cost += cost;
       st.energy_nw += e_step;
@@ -975,6 +1006,24 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     }
   }
   if (prev_h >= 0) st.gco2 += (double)st.e_hour * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
+  if (det && prev_h >= 0) {
+    for (int p = 0; p < w->n_pools; ++p) {
+      det->pool_gco2[p] += (double)pool_eh[p] * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
+      int cnt = 0;
+      for (int n = 0; n < NN; ++n) cnt += st.nodes[n].used && st.nodes[n].pool == p;
+      det->pool_final_nodes[p] = cnt;
+      det->pool_launches[p] = st.pool_launches[p];
+    }
+    det->base_gco2 += (double)base_eh * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
+    for (int d = 0; d < D; ++d) {
+      int rd = 0;
+      for (int n = 0; n < NN; ++n)
+        if (st.nodes[n].used && st.nodes[n].ready_step <= w->n_steps - 1) rd += st.nodes[n].pods[d];
+      det->desired[d] = st.dep[d].replicas;
+      det->ready[d] = rd;
+      det->pending[d] = st.dep[d].replicas - rd;
+    }
+  }
   int reps = 0, nodes = 0;
   for (int d = 0; d < D; ++d) reps += st.dep[d].replicas;
   for (int n = 0; n < NN; ++n) nodes += st.nodes[n].used;
@@ -1000,17 +1049,23 @@ typedef struct {
   const int32_t* load;
   ccka_results* out;
   ccka_traj_rec* traj;
+  ccka_detail* detail;
   int64_t lo, hi;
 } o_job;
 
 static void* o_worker(void* arg) {
   o_job* j = (o_job*)arg;
-  for (int64_t i = j->lo; i < j->hi; ++i) o_run_one(j->e, j->sc, j->load, i, j->sc->n, j->out, j->traj);
+  for (int64_t i = j->lo; i < j->hi; ++i) o_run_one(j->e, j->sc, j->load, i, j->sc->n, j->out, j->traj, j->detail ? &j->detail[i] : NULL);
   return NULL;
 }
 
 int ccka_oracle_rollout(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
                         ccka_results* out, ccka_traj_rec* traj, int32_t n_threads) {
+  return ccka_oracle_rollout_detail(w, sc, load, out, traj, NULL, n_threads);
+}
+
+int ccka_oracle_rollout_detail(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
+                               ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, int32_t n_threads) {
   if (!w || !sc || !load || !out || w->n_deploy < 1 || w->n_deploy > CCKA_MAX_DEPLOY ||
       w->max_nodes < 1 || w->max_nodes > CCKA_MAX_NODES || w->n_types < 1 || w->n_zones < 1 ||
       w->n_zones > CCKA_MAX_ZONES || w->n_pools < 1 || w->n_pools > CCKA_MAX_POOLS)
@@ -1049,6 +1104,7 @@ int ccka_oracle_rollout(const ccka_world* w, const ccka_scenarios* sc, const int
     jobs[k].load = load;
     jobs[k].out = out;
     jobs[k].traj = traj;
+    jobs[k].detail = detail;
     jobs[k].lo = sc->n * k / n_threads;
     jobs[k].hi = sc->n * (k + 1) / n_threads;
   }

@@ -24,6 +24,11 @@ extern "C" {
 int ccka_oracle_rollout(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
                         ccka_results* out, ccka_traj_rec* traj, int32_t n_threads);
 
+/* The same, also filling detail[sc->n] (ccka_detail, per pool / base group /
+ * deployment) when detail is non-NULL. */
+int ccka_oracle_rollout_detail(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
+                               ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, int32_t n_threads);
+
 /* Serial totals over results (fixed scenario order). */
 void ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* out);
 

@@ -48,6 +48,10 @@ def lib():
         L.ccka_oracle_rollout.argtypes = [C.POINTER(abi.World), C.POINTER(abi.Scenarios),
                                           C.POINTER(C.c_int32), C.POINTER(abi.Results),
                                           C.POINTER(abi.TrajRec), C.c_int32]
+        L.ccka_oracle_rollout_detail.restype = C.c_int
+        L.ccka_oracle_rollout_detail.argtypes = [C.POINTER(abi.World), C.POINTER(abi.Scenarios),
+                                                 C.POINTER(C.c_int32), C.POINTER(abi.Results),
+                                                 C.POINTER(abi.TrajRec), C.c_void_p, C.c_int32]
         L.ccka_oracle_totals.argtypes = [C.POINTER(abi.Results), C.c_int64, C.POINTER(abi.Totals)]
         L.ccka_oracle_hpa_resource_proposal.restype = C.c_int32
         L.ccka_oracle_hpa_resource_proposal.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_int32,
@@ -75,24 +79,32 @@ def gen_load(gen, T, D, n, first_id=0):
     return out
 
 
-def rollout(spec, scen, load, traj=False, threads=1):
-    """Run the oracle; returns (results dict, trajectory array or None)."""
+def rollout(spec, scen, load, traj=False, threads=1, detail=False):
+    """Run the oracle; returns (results dict, trajectory array or None), plus
+    the ccka_detail records as a third element when detail=True."""
     w = spec.to_c()
+    return rollout_world(w, scen, load, traj, threads, detail, spec=spec)
+
+
+def rollout_world(world, scen, load, traj=False, threads=1, detail=False, spec=None):
+    """Like rollout() but from a raw abi.World (e.g. built by libccka_host)."""
     s = scen.to_c()
     load = np.ascontiguousarray(load, np.int32)
-    cols = scen.n_traces if scen.n_traces > 0 else scen.n
-    assert load.shape == (spec.n_steps, len(spec.deploys), cols), load.shape
+    if spec is not None:
+        cols = scen.n_traces if scen.n_traces > 0 else scen.n
+        assert load.shape == (spec.n_steps, len(spec.deploys), cols), load.shape
     arrays, r = alloc_results(scen.n)
     tr = None
     trp = None
     if traj:
-        tr = np.zeros((spec.n_steps, scen.n), TRAJ_DTYPE)
+        tr = np.zeros((world.n_steps, scen.n), TRAJ_DTYPE)
         trp = tr.ctypes.data_as(C.POINTER(abi.TrajRec))
-    rc = lib().ccka_oracle_rollout(C.byref(w), C.byref(s), load.ctypes.data_as(C.POINTER(C.c_int32)),
-                                   C.byref(r), trp, threads)
+    det = np.zeros(scen.n, abi.detail_dtype()) if detail else None
+    rc = lib().ccka_oracle_rollout_detail(C.byref(world), C.byref(s), load.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          C.byref(r), trp, det.ctypes.data if detail else None, threads)
     if rc != 0:
         raise abi.CckaError(f"oracle rollout failed: {rc}")
-    return arrays, tr
+    return (arrays, tr, det) if detail else (arrays, tr)
 
 
 def totals(arrays, n):
@@ -102,23 +114,6 @@ def totals(arrays, n):
     t = abi.Totals()
     lib().ccka_oracle_totals(C.byref(r), n, C.byref(t))
     return t
-
-
-def rollout_world(world, scen, load, traj=False, threads=1):
-    """Like rollout() but from a raw abi.World (e.g. built by libccka_host)."""
-    s = scen.to_c()
-    load = np.ascontiguousarray(load, np.int32)
-    arrays, r = alloc_results(scen.n)
-    tr = None
-    trp = None
-    if traj:
-        tr = np.zeros((world.n_steps, scen.n), TRAJ_DTYPE)
-        trp = tr.ctypes.data_as(C.POINTER(abi.TrajRec))
-    rc = lib().ccka_oracle_rollout(C.byref(world), C.byref(s), load.ctypes.data_as(C.POINTER(C.c_int32)),
-                                   C.byref(r), trp, threads)
-    if rc != 0:
-        raise abi.CckaError(f"oracle rollout failed: {rc}")
-    return arrays, tr
 
 
 # ---------------------------------------------------------------------------
