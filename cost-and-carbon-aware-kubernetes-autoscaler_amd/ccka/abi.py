@@ -17,6 +17,10 @@ MAX_POOLS = 4
 MAX_DEPLOY = 16
 MAX_NODES = 16
 HIST = 8
+HPA_MAX_POLICIES = 4
+HPA_MAX_WINDOW_S = 3600
+HPA_MAX_PERIOD_S = 1800
+HPA_HIST_MAX = 360
 
 CAP_SPOT, CAP_OD = 1, 2
 POLICY_KEEP, WHEN_EMPTY, WHEN_EMPTY_OR_UNDERUTILIZED = 0, 1, 2
@@ -33,7 +37,7 @@ STATUS = {0: "OK", -1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ERCCL",
 class ItType(C.Structure):
     _fields_ = [("vcpu", C.c_int32), ("alloc_cpu_m", C.c_int32), ("alloc_mem_mi", C.c_int32),
                 ("max_pods", C.c_int32), ("idle_nw", C.c_int64), ("dyn_nw_per_m", C.c_int64),
-                ("p_ref_w", C.c_double), ("_reserved", C.c_double)]
+                ("p_ref_w", C.c_double), ("mem_mi", C.c_int32), ("_pad", C.c_int32)]
 
 
 class PoolPatch(C.Structure):
@@ -43,7 +47,7 @@ class PoolPatch(C.Structure):
 
 class Pool(C.Structure):
     _fields_ = [("limit_cpu_m", C.c_int32), ("budget_pct", C.c_int32), ("base", PoolPatch),
-                ("profile", PoolPatch * 3)]
+                ("profile", PoolPatch * 3), ("limit_mem_mi", C.c_int32), ("_pad", C.c_int32)]
 
 
 class HpaPolicy(C.Structure):
@@ -52,7 +56,7 @@ class HpaPolicy(C.Structure):
 
 class HpaRules(C.Structure):
     _fields_ = [("select", C.c_int32), ("n_policies", C.c_int32), ("stab_window_s", C.c_int32),
-                ("_pad", C.c_int32), ("policies", HpaPolicy * 2)]
+                ("_pad", C.c_int32), ("policies", HpaPolicy * HPA_MAX_POLICIES)]
 
 
 class Deployment(C.Structure):
@@ -78,7 +82,8 @@ class World(C.Structure):
                 ("base_util", C.c_double), ("carbon_weight", C.c_double),
                 ("pdb_min_available_pct", C.c_int32), ("peak_start_min", C.c_int32),
                 ("peak_end_min", C.c_int32), ("peak_switch", C.c_int32),
-                ("reset_ca_s", C.c_int32), ("disrupt_ext", C.c_int32)]
+                ("reset_ca_s", C.c_int32), ("disrupt_ext", C.c_int32), ("hpa_sync_s", C.c_int32),
+                ("_pad2", C.c_int32)]
 
 
 class Scenarios(C.Structure):

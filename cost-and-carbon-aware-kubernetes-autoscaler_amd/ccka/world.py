@@ -118,6 +118,7 @@ class Catalog:
             t.idle_nw = llround(p_idle * 1e9)
             t.dyn_nw_per_m = llround(p_dyn * 1e9 / float(t.alloc_cpu_m))
             t.p_ref_w = p_idle + 0.5 * p_dyn
+            t.mem_mi = int(self.mem_gib[i] * 1024)
         return arr
 
     def index(self, name):
@@ -225,13 +226,13 @@ def reference_pools(offpeak_zones=("us-east-2a",), peak_zones=("us-east-2c",),
     allz = zone_mask(all_zones)
     off, pk = zone_mask(offpeak_zones), zone_mask(peak_zones)
     od = abi.Pool()
-    od.limit_cpu_m, od.budget_pct = -1, 10
+    od.limit_cpu_m, od.budget_pct, od.limit_mem_mi = -1, 10, -1
     od.base = patch(abi.WHEN_EMPTY_OR_UNDERUTILIZED, 0, allz, abi.CAP_OD)
     od.profile[abi.PROFILE_RESET] = patch(abi.WHEN_EMPTY, 30)
     od.profile[abi.PROFILE_OFFPEAK] = patch(abi.WHEN_EMPTY, 60, off, abi.CAP_OD)
     od.profile[abi.PROFILE_PEAK] = patch(abi.WHEN_EMPTY, 120, pk, abi.CAP_OD)
     sp = abi.Pool()
-    sp.limit_cpu_m, sp.budget_pct = -1, 10
+    sp.limit_cpu_m, sp.budget_pct, sp.limit_mem_mi = -1, 10, -1
     sp.base = patch(abi.WHEN_EMPTY_OR_UNDERUTILIZED, 0, allz, abi.CAP_SPOT | abi.CAP_OD)
     sp.profile[abi.PROFILE_RESET] = patch(abi.WHEN_EMPTY, 30)
     sp.profile[abi.PROFILE_OFFPEAK] = patch(abi.WHEN_EMPTY_OR_UNDERUTILIZED, -1, off,
@@ -295,6 +296,7 @@ class WorldSpec:
     carbon_weight: float = 0.0
     drift: int = 0                 # CCKA_DISRUPT_DRIFT
     replace: int = 0               # CCKA_DISRUPT_REPLACE
+    hpa_sync_s: int = 0            # HPA decision period: 0/60 = once per step; 10/15/20/30 = sub-steps
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -341,6 +343,7 @@ class WorldSpec:
         w.peak_switch = self.peak_switch
         w.reset_ca_s = self.reset_ca_s
         w.disrupt_ext = (abi.DISRUPT_DRIFT if self.drift else 0) | (abi.DISRUPT_REPLACE if self.replace else 0)
+        w.hpa_sync_s = self.hpa_sync_s
         return w
 
 

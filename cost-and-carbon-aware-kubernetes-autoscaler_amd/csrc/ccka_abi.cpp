@@ -73,6 +73,10 @@ struct ccka_ctx {
   bool d1_ready = false;     // scenario-dependent part prepared
   bool d1_ok = false;        // world + scenarios qualify
   bool sc_maxr_ok = true;
+  int sc_dstab_max = -1;      // largest per-scenario down_stab_s override (-1: none given)
+  // HPA decision history in HBM for long windows / sub-steps (general kernel)
+  int2* d_hist = nullptr;
+  int64_t hist_count = 0;
   uint32_t sc_capsel_or = 0;  // OR of the per-scenario cap_sel overrides (0: none given)
   int sc_pswitch_any = -1;    // any per-scenario peak_switch set (-1: none given)
   D1Params d1{};
@@ -171,6 +175,17 @@ static int pod_cap(const ccka_itype& t, int rc, int rm) {
   return f;
 }
 
+// decisions of the register history rings (8 entries at one decision per
+// step) cover the rules: the fast paths; otherwise the HBM history
+static bool rules_fit_ring(const ccka_hpa_rules& r) {
+  if (r.n_policies > 2 || r.stab_window_s > CCKA_HIST * CCKA_STEP_SECONDS) return false;
+  for (int i = 0; i < r.n_policies; ++i)
+    if (r.policies[i].period_s > CCKA_HIST * CCKA_STEP_SECONDS) return false;
+  return true;
+}
+
+static int hist_entries(int window_s, int sync_s) { return window_s > sync_s ? (window_s - 1) / sync_s : 0; }
+
 static D1Rule d1_rule(const ccka_hpa_rules& r, bool up) {
   auto wm = [](int w) {
     int m = 0;
@@ -217,7 +232,10 @@ static int d1_check_world(ccka_ctx* c) {
   // drift / replacement run on the general kernel unless d1_prepare proves
   // them inert for these scenarios (d1_disrupt_inert)
   for (int q = 0; q < w.n_pools; ++q)
-    if (w.pools[q].limit_cpu_m >= 0) return CCKA_OK;
+    if (w.pools[q].limit_cpu_m >= 0 || w.pools[q].limit_mem_mi >= 0) return CCKA_OK;
+  // one HPA decision per step over the 8-entry register rings
+  if ((w.hpa_sync_s != 0 && w.hpa_sync_s != CCKA_STEP_SECONDS) || !rules_fit_ring(dp.up) || !rules_fit_ring(dp.down))
+    return CCKA_OK;
   if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
       dp.limit_cpu_m > 65535 ||
       dp.min_replicas < 0 || dp.max_replicas < 0 || dp.max_replicas > D1_REC_SAT || dp.replicas0 > D1_REC_SAT)
@@ -351,6 +369,7 @@ static int d1_prepare(ccka_ctx* c) {
   c->d1_ready = true;
   c->d1_ok = false;
   if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_inert(c)) return CCKA_OK;
+  if (c->sc_dstab_max > CCKA_HIST * CCKA_STEP_SECONDS) return CCKA_OK;  // beyond the register ring
   const size_t n = (size_t)c->N;
   std::vector<double> wl;
   std::vector<uint8_t> wci;
@@ -461,7 +480,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
   dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_ggather); dfree(c->d_gcounts); dfree(c->d_gn);
-  dfree(c->d_gflags); dfree(c->d_gfront);
+  dfree(c->d_gflags); dfree(c->d_gfront); dfree(c->d_hist);
   dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -471,17 +490,21 @@ void ccka_close(ccka_ctx* c) {
   delete c;
 }
 
+// autoscaling/v2 ranges: stabilizationWindowSeconds 0..3600, periodSeconds
+// 1..1800 (0 accepted: an empty period), up to CCKA_HPA_MAX_POLICIES policies
 static bool rules_ok(const ccka_hpa_rules& r) {
-  if (r.select < 0 || r.select > 2 || r.n_policies < 0 || r.n_policies > 2) return false;
-  if (r.stab_window_s < 0 || r.stab_window_s > CCKA_HIST * CCKA_STEP_SECONDS) return false;
+  if (r.select < 0 || r.select > 2 || r.n_policies < 0 || r.n_policies > CCKA_HPA_MAX_POLICIES) return false;
+  if (r.stab_window_s < 0 || r.stab_window_s > CCKA_HPA_MAX_WINDOW_S) return false;
   for (int i = 0; i < r.n_policies; ++i) {
     const ccka_hpa_policy& p = r.policies[i];
     if ((p.type != CCKA_HPA_PODS && p.type != CCKA_HPA_PERCENT) || p.value < 0 || p.period_s < 0 ||
-        p.period_s > CCKA_HIST * CCKA_STEP_SECONDS)
+        p.period_s > CCKA_HPA_MAX_PERIOD_S)
       return false;
   }
   return true;
 }
+
+
 
 int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
   if (!c || !w) return CCKA_EINVAL;
@@ -517,9 +540,14 @@ int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
          (w->deploy[d - 1].scaler != CCKA_SCALER_KEDA && w->deploy[d - 1].scaler != CCKA_SCALER_KEDA_TRIGGER)))
       return fail(c, CCKA_EINVAL, "KEDA trigger %d must follow a KEDA deployment and own no pods", d);
     if (!rules_ok(dp.up) || !rules_ok(dp.down))
-      return fail(c, CCKA_EINVAL, "deployment %d behavior outside the %d s history", d,
-                  CCKA_HIST * CCKA_STEP_SECONDS);
+      return fail(c, CCKA_EINVAL, "deployment %d behavior outside autoscaling/v2 ranges (window <= %d s, period <= %d s, "
+                  "<= %d policies)", d, CCKA_HPA_MAX_WINDOW_S, CCKA_HPA_MAX_PERIOD_S, CCKA_HPA_MAX_POLICIES);
   }
+  if (w->hpa_sync_s != 0 && w->hpa_sync_s != 10 && w->hpa_sync_s != 15 && w->hpa_sync_s != 20 &&
+      w->hpa_sync_s != 30 && w->hpa_sync_s != 60)
+    return fail(c, CCKA_EINVAL, "hpa_sync_s must be 0, 10, 15, 20, 30 or 60");
+  for (int q = 0; q < w->n_pools; ++q)
+    if (w->pools[q].limit_mem_mi < -1) return fail(c, CCKA_EINVAL, "pool %d limit_mem_mi invalid", q);
   c->hw = *w;
   const int K = w->n_types, Z = w->n_zones, R = w->n_regions;
   int rc;
@@ -598,10 +626,13 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   if (sc->target_util_pct)
     for (size_t i = 0; i < n; ++i)
       if (sc->target_util_pct[i] <= 0) return fail(c, CCKA_EINVAL, "target_util_pct must be > 0");
+  c->sc_dstab_max = -1;
   if (sc->down_stab_s)
-    for (size_t i = 0; i < n; ++i)
-      if (sc->down_stab_s[i] < 0 || sc->down_stab_s[i] > CCKA_HIST * CCKA_STEP_SECONDS)
-        return fail(c, CCKA_EINVAL, "down_stab_s outside the history window");
+    for (size_t i = 0; i < n; ++i) {
+      if (sc->down_stab_s[i] < 0 || sc->down_stab_s[i] > CCKA_HPA_MAX_WINDOW_S)
+        return fail(c, CCKA_EINVAL, "down_stab_s outside 0..%d s", CCKA_HPA_MAX_WINDOW_S);
+      c->sc_dstab_max = std::max<int>(c->sc_dstab_max, sc->down_stab_s[i]);
+    }
   int rc;
   if ((rc = dupload(c, c->d_region, sc->region, n)) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_target, sc->target_util_pct, n)) != CCKA_OK) return rc;
@@ -785,6 +816,37 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     }
     HIPCHK(c, hipMemsetAsync(c->d_detail, 0, (size_t)c->N * sizeof(DetailDev), c->stream));
     k.detail = c->d_detail;
+  }
+  // HPA decisions: one per step over the register rings, or nsub per step /
+  // long windows / > 2 policies over the HBM history (SEMANTICS 3.C)
+  k.sync_s = w.hpa_sync_s > 0 ? w.hpa_sync_s : CCKA_STEP_SECONDS;
+  k.nsub = CCKA_STEP_SECONDS / k.sync_s;
+  {
+    bool fit = k.nsub == 1 && c->sc_dstab_max <= CCKA_HIST * CCKA_STEP_SECONDS;
+    int hl = 0;
+    for (int d = 0; d < w.n_deploy; ++d) {
+      const ccka_deployment& dp = w.deploy[d];
+      if (dp.scaler != CCKA_SCALER_HPA && dp.scaler != CCKA_SCALER_KEDA) continue;
+      fit = fit && rules_fit_ring(dp.up) && rules_fit_ring(dp.down);
+      int dstab = dp.down.stab_window_s;
+      if (dp.scaler == CCKA_SCALER_HPA && c->sc_dstab_max >= 0) dstab = std::max(dstab, c->sc_dstab_max);
+      hl = std::max({hl, hist_entries(dp.up.stab_window_s, k.sync_s), hist_entries(dstab, k.sync_s)});
+      for (const ccka_hpa_rules* r : {&dp.up, &dp.down})
+        for (int q = 0; q < r->n_policies; ++q) hl = std::max(hl, hist_entries(r->policies[q].period_s, k.sync_s));
+    }
+    k.hlen = fit ? 0 : std::max(hl, 1);
+    k.hist = nullptr;
+    if (k.hlen) {
+      const int64_t cnt = (int64_t)k.hlen * w.n_deploy * c->N;
+      if (c->hist_count < cnt) {
+        dfree(c->d_hist);
+        if (hipMalloc((void**)&c->d_hist, (size_t)cnt * sizeof(int2)) != hipSuccess)
+          return fail(c, CCKA_ENOMEM, "HPA history alloc (%lld entries)", (long long)cnt);
+        c->hist_count = cnt;
+      }
+      HIPCHK(c, hipMemsetAsync(c->d_hist, 0, (size_t)cnt * sizeof(int2), c->stream));
+      k.hist = c->d_hist;
+    }
   }
   k.N = c->N;
   k.NL = load_cols(c);

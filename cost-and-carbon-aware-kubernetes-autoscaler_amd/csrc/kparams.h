@@ -48,6 +48,8 @@ struct KParams {
   uint32_t* hash;
   ccka_traj_rec* traj;  // nullable
   DetailDev* detail;    // nullable: per-scenario summary breakdown (ccka_set_detail)
+  int2* hist;           // HBM decision history [hlen][D][N] {rec + 1 (0: none), delta}; hlen 0: register rings
+  int32_t hlen, nsub, sync_s, _hpad;
   int64_t N;
   int64_t NL;           // load columns: N, or the shared trace count
   int64_t trace_mod;    // 0: column = scenario; else column = (first_id + i) % trace_mod

@@ -174,18 +174,20 @@ __device__ __forceinline__ bool type_offered(const Lds& L, int rl, int k, uint32
   return false;
 }
 
-__device__ __forceinline__ bool limit_ok(const Lds& L, int k, int use, int limit) {
-  return limit < 0 || use + L.types[k].vcpu * 1000 <= limit;
+// NodePool spec.limits: a new node of type k keeps the pool's CPU (millicores)
+// and memory (MiB) capacity within the limits (-1: none)
+__device__ __forceinline__ bool limit_ok(const Lds& L, int k, int use, int limit, int usem, int limitm) {
+  return (limit < 0 || use + L.types[k].vcpu * 1000 <= limit) && (limitm < 0 || usem + L.types[k].mem_mi <= limitm);
 }
 
 // wave-cooperative j (max additional pods of d over candidate types). All
 // arguments are wave-uniform.
 template <int DMAX>
 __device__ int wave_claim_j(const Lds& L, int rl, uint32_t zm, uint32_t cm, int s_cpu, int s_mem,
-                            int s_pods, int rc, int rm, int use, int limit, int lane) {
+                            int s_pods, int rc, int rm, int use, int limit, int usem, int limitm, int lane) {
   int best = 0;
   for (int k = lane; k < L.K; k += WAVE) {
-    if (!limit_ok(L, k, use, limit)) continue;
+    if (!limit_ok(L, k, use, limit, usem, limitm)) continue;
     const int f = type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, rc, rm);
     if (f <= best) continue;
     if (!type_offered(L, rl, k, zm, cm)) continue;
@@ -197,12 +199,13 @@ __device__ int wave_claim_j(const Lds& L, int rl, uint32_t zm, uint32_t cm, int 
 // wave-cooperative launch decision; returns packed idx (k*Z+z)*2+c or -1.
 template <int DMAX>
 __device__ int wave_launch(const Lds& L, int rl, uint32_t zm, uint32_t cm, int s_cpu, int s_mem,
-                           int s_pods, int use, int limit, double wc1000, double ci_gpwh, int lane) {
+                           int s_pods, int use, int limit, int usem, int limitm, double wc1000, double ci_gpwh,
+                           int lane) {
   bool spot_only = false;
   if (cm & CCKA_CAP_SPOT) {
     bool any = false;
     for (int k = lane; k < L.K && !any; k += WAVE) {
-      if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, use, limit)) continue;
+      if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, use, limit, usem, limitm)) continue;
       for (int z = 0; z < L.Z; ++z)
         if ((zm >> z & 1u) && tprice(L, rl, k, z, 0) > 0) { any = true; break; }
     }
@@ -211,7 +214,7 @@ __device__ int wave_launch(const Lds& L, int rl, uint32_t zm, uint32_t cm, int s
   double bs = __builtin_inf();
   int bi = 0x7fffffff;
   for (int k = lane; k < L.K; k += WAVE) {
-    if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, use, limit)) continue;
+    if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, use, limit, usem, limitm)) continue;
     const double carbon = L.types[k].p_ref_w * ci_gpwh;
     for (int z = 0; z < L.Z; ++z) {
       if (!(zm >> z & 1u)) continue;
@@ -322,6 +325,68 @@ __device__ __forceinline__ int rate_limit(const Rule& R, bool up, int cur, const
     res = (up == min_sel) ? min(res, pr) : max(res, pr);
   }
   return (int)res;
+}
+
+// decision-history entries inside a window / period: entry k is (k + 1) * sync_s old
+__device__ __forceinline__ int hist_n(int window_s, int sync_s) { return window_s > sync_s ? (window_s - 1) / sync_s : 0; }
+
+// replicas added / removed by the scaler over the n newest HBM history entries
+__device__ __forceinline__ void hist_sums(const int2* ring, int hpos, int hlen, int64_t stride, int n, int* add,
+                                          int* rem) {
+  int a = 0, r = 0, idx = hpos;
+  for (int k = 0; k < n; ++k) {
+    idx = idx == 0 ? hlen - 1 : idx - 1;
+    const int dl = ring[(int64_t)idx * stride].y;
+    a += max(dl, 0);
+    r += max(-dl, 0);
+  }
+  *add = a;
+  *rem = r;
+}
+
+// rate limit of one direction over the HBM history (one policy at a time:
+// few live registers on this rare path)
+__device__ int rate_long(const ccka_hpa_rules* R, bool up, int cur, int sync_s, const int2* ring, int hpos, int hlen,
+                         int64_t stride) {
+  if (R->select == CCKA_SELECT_DISABLED) return cur;
+  const bool min_sel = R->select == CCKA_SELECT_MIN;
+  long long res = (up == min_sel) ? 0x7fffffffLL : -0x80000000LL;
+  for (int q = 0; q < R->n_policies; ++q) {
+    const ccka_hpa_policy& P = R->policies[q];
+    int add, rem;
+    hist_sums(ring, hpos, hlen, stride, min(hist_n(P.period_s, sync_s), hlen), &add, &rem);
+    const long long pst = (long long)cur - add + rem;
+    long long pr;
+    if (P.type == CCKA_HPA_PODS) pr = up ? pst + P.value : pst - P.value;
+    else if (up) pr = (int)ceil((double)pst * (1.0 + (double)P.value / 100.0));
+    else pr = (int)((double)pst * (1.0 - (double)P.value / 100.0));
+    res = (up == min_sel) ? min(res, pr) : max(res, pr);
+  }
+  return (int)res;
+}
+
+// HPA behavior (stabilisation + rate limits) over the HBM decision history:
+// windows up to 3600 s, up to 4 policies per direction, hpa_sync_s sub-steps
+// (SEMANTICS 3.C). Entry k of this (deployment, scenario) lives at
+// ring[((hpos - 1 - k) mod hlen) * stride].
+__device__ int behavior_long(const ccka_hpa_rules* up, const ccka_hpa_rules* dn, int dstab, int sync_s, int cur,
+                             int proposal, int minr, int mx, const int2* ring, int hpos, int hlen, int64_t stride) {
+  const int nu = min(hist_n(up->stab_window_s, sync_s), hlen), nd = min(hist_n(dstab, sync_s), hlen);
+  int upr = proposal, dnr = proposal, idx = hpos;
+  for (int k = 0; k < max(nu, nd); ++k) {
+    idx = idx == 0 ? hlen - 1 : idx - 1;
+    const int rx = ring[(int64_t)idx * stride].x;
+    if (rx) {
+      if (k < nu) upr = min(upr, rx - 1);
+      if (k < nd) dnr = max(dnr, rx - 1);
+    }
+  }
+  int rc = max(cur, upr);
+  rc = min(rc, dnr);
+  int lo = minr, hi = mx;
+  if (rc > cur) hi = min(hi, max(rate_long(up, true, cur, sync_s, ring, hpos, hlen, stride), cur));
+  else if (rc < cur) lo = max(lo, min(rate_long(dn, false, cur, sync_s, ring, hpos, hlen, stride), cur));
+  return rc < lo ? lo : (rc > hi ? hi : rc);
 }
 
 template <int DMAX, int MAXN>
@@ -473,6 +538,15 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   };
 
   uint32_t used = 0, rdy = 0;
+  // memory capacity (MiB) of pool q's nodes: recounted where a limits.memory
+  // applies (rare) instead of a register per pool
+  auto pool_mem = [&](int q) {
+    int m = 0;
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n)
+      if (((used >> n) & 1u) && ni_pool(ninfo[n]) == q) m += L.types[ni_type(ninfo[n])].mem_mi;
+    return m;
+  };
   const uint32_t slot_mask = NN >= 32 ? 0xFFFFFFFFu : ((1u << NN) - 1u);
   int next_ready = 0x7fffffff;  // earliest ready_step among not-ready nodes
   int nsp = 0, nod = 0;         // Karpenter nodes by capacity type
@@ -493,6 +567,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       (long long)base_nodes * (bt.idle_nw + bt.dyn_nw_per_m * (long long)(gw->base_util * (double)bt.alloc_cpu_m));
   const int ps = gw->peak_start_min, pe = gw->peak_end_min;
   const int delay = gw->provision_delay_steps;
+  int hpos = 0;  // HBM history write position (p.hlen > 0)
 
   // load samples are software-pipelined one step ahead: the HBM latency of
   // step t+1's coalesced read hides behind step t's decision work
@@ -600,7 +675,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           if (x.cap_mask) pcm[q] = x.cap_mask;
         }
       }
-      // ---- C. scalers ----
+      // ---- C. scalers: nsub decisions on the step's metric sample ----
+      for (int sub = 0; sub < p.nsub; ++sub) {
+      if (sub > 0) {
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; kact_any[d] = false; }
+      }
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d >= D) break;
@@ -677,7 +757,13 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             }
           }
         }
-        if (do_behavior && !(p.ablate & 8)) {
+        if (do_behavior && !(p.ablate & 8) && p.hlen) {
+          ran = true;
+          const ccka_deployment& gd = gw->deploy[d];
+          const int dstab = p.down_stab && dp.scaler == CCKA_SCALER_HPA ? (int)p.down_stab[i] : gd.down.stab_window_s;
+          desired = behavior_long(&gd.up, &gd.down, dstab, p.sync_s, cur, proposal, minr, mx, p.hist + (int64_t)d * p.N + i,
+                                  hpos, p.hlen, (int64_t)D * p.N);
+        } else if (do_behavior && !(p.ablate & 8)) {
           ran = true;
           // stabilisation over the valid records inside each window
           const uint32_t upm = recv[d] & (uint32_t)dp.up.stab_mask;
@@ -695,15 +781,24 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           else if (rc < cur) lo = max(lo, min(rate_limit(dp.dn, false, cur, delta[d]), cur));
           desired = rc < lo ? lo : (rc > hi ? hi : rc);
         }
-        // shift history rings; entry 0 = this step
+        if (p.hlen) {  // HBM history: this decision at hpos
+          int2 e;
+          e.x = ran ? proposal + 1 : 0;
+          e.y = (hpa_path && desired != cur) ? desired - cur : 0;
+          p.hist[((int64_t)hpos * D + d) * p.N + i] = e;
+        } else {
+          // shift history rings; entry 0 = this step
 #pragma unroll
-        for (int k = CCKA_HIST - 1; k > 0; --k) { rec[d][k] = rec[d][k - 1]; delta[d][k] = delta[d][k - 1]; }
-        rec[d][0] = ran ? proposal : 0;
-        recv[d] = ((recv[d] << 1) | (ran ? 1u : 0u)) & 0xFFu;
-        delta[d][0] = (hpa_path && desired != cur) ? desired - cur : 0;
+          for (int k = CCKA_HIST - 1; k > 0; --k) { rec[d][k] = rec[d][k - 1]; delta[d][k] = delta[d][k - 1]; }
+          rec[d][0] = ran ? proposal : 0;
+          recv[d] = ((recv[d] << 1) | (ran ? 1u : 0u)) & 0xFFu;
+          delta[d][0] = (hpa_path && desired != cur) ? desired - cur : 0;
+        }
         if (desired != cur) g_dirty = true;  // PDB expectation changed
         replicas[d] = desired;
       }
+      if (p.hlen) hpos = hpos + 1 == p.hlen ? 0 : hpos + 1;
+      }  // sub-steps
       // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
@@ -792,6 +887,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         const double lci = rdld(ci_gpwh, ld);
         uint32_t lfree = rdlu(free_mask, ld);
         int use0[CCKA_MAX_POOLS], usenow[CCKA_MAX_POOLS];
+        // pool memory in use (limits.memory only): lane ld's slots, launches of
+        // this step included (they update its slots as they happen)
+        auto mem_now = [&](int q) { return w->pools[q].limit_mem_mi >= 0 ? rdl(pool_mem(q), ld) : 0; };
         uint32_t lzm[CCKA_MAX_POOLS], lcm[CCKA_MAX_POOLS];
 #pragma unroll
         for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
@@ -822,7 +920,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
             for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) climit = plimit[q];
             const int j = wave_claim_j<DMAX>(L, lrl, (uint32_t)cl[2], cm, cl[4], cl[5], cl[6], rc, rm,
-                                             use0[cpool], climit, lane);
+                                             use0[cpool], climit, mem_now(cpool), w->pools[cpool].limit_mem_mi, lane);
             if (j <= 0) continue;
             const int k = min(j, rem);
             __builtin_amdgcn_wave_barrier();
@@ -840,7 +938,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             for (int q = 0; q < NP; ++q) {
               const uint32_t cm = lcm[q] & csel;
               if (!cm) continue;
-              const int j = wave_claim_j<DMAX>(L, lrl, lzm[q], cm, 0, 0, 0, rc, rm, use0[q], plimit[q], lane);
+              const int j = wave_claim_j<DMAX>(L, lrl, lzm[q], cm, 0, 0, 0, rc, rm, use0[q], plimit[q], mem_now(q),
+                                               w->pools[q].limit_mem_mi, lane);
               if (j > 0) { chosen = q; jj = j; break; }
             }
             if (chosen < 0) break;
@@ -869,7 +968,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
           for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) climit = plimit[q];
           const int bi = wave_launch<DMAX>(L, lrl, (uint32_t)cl[2], (uint32_t)cl[1], cl[4], cl[5],
-                                           cl[6], usenow[cpool], climit, lwc, lci, lane);
+                                           cl[6], usenow[cpool], climit, mem_now(cpool), w->pools[cpool].limit_mem_mi,
+                                           lwc, lci, lane);
           if (bi < 0) continue;
           const int bc = bi & 1, bz = (bi >> 1) % Z, bk = (bi >> 1) / Z;
           const int vcpu_m = L.types[bk].vcpu * 1000;
@@ -901,7 +1001,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             if (now_ready) rdy |= 1u << slot;
             else next_ready = min(next_ready, t + delay);
 #pragma unroll
-            for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) puse[q] += vcpu_m;
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q)
+              if (q == cpool) puse[q] += vcpu_m;
             if (bc == 0) nsp++; else nod++;
             burn += price;
             launches++;
@@ -957,12 +1058,12 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         };
         // cheapest single offering (price, k, z, c) that holds the sums under a
         // pool's zone / capacity-type masks and CPU limit
-        auto find_offer = [&](uint32_t zm, uint32_t cm, int use, int limit, int s_cpu, int s_mem, int s_pods,
-                              int& bk, int& bz, int& bc, int& bpr) {
+        auto find_offer = [&](uint32_t zm, uint32_t cm, int use, int limit, int usem, int limitm, int s_cpu, int s_mem,
+                              int s_pods, int& bk, int& bz, int& bc, int& bpr) {
           bk = -1; bz = 0; bc = 0; bpr = 0;
           for (int k = 0; k < L.K; ++k) {
             if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
-            if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+            if (!limit_ok(L, k, use, limit, usem, limitm)) continue;
             for (int z = 0; z < L.Z; ++z) {
               if (!(zm >> z & 1u)) continue;
 #pragma unroll
@@ -977,14 +1078,14 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         // the F2 launch rule for one NodeClaim, per lane (SEMANTICS 3.F): spot
         // offerings only when spot is allowed and any is feasible; argmin of
         // (score, k, z, c), score = price + carbon weight * 1000 * p_ref_w * ci
-        auto lane_launch = [&](uint32_t zm, uint32_t cm, int use, int limit, int s_cpu, int s_mem, int s_pods,
-                               int& bk, int& bz, int& bc, int& bpr) {
+        auto lane_launch = [&](uint32_t zm, uint32_t cm, int use, int limit, int usem, int limitm, int s_cpu,
+                               int s_mem, int s_pods, int& bk, int& bz, int& bc, int& bpr) {
           bk = -1; bz = 0; bc = 0; bpr = 0;
           bool spot_only = false;
           if (cm & CCKA_CAP_SPOT) {
             for (int k = 0; k < L.K && !spot_only; ++k) {
               if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
-              if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+              if (!limit_ok(L, k, use, limit, usem, limitm)) continue;
               for (int z = 0; z < L.Z; ++z)
                 if ((zm >> z & 1u) && tprice(L, rl, k, z, 0) > 0) { spot_only = true; break; }
             }
@@ -992,7 +1093,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           double bs = 0.0;
           for (int k = 0; k < L.K; ++k) {
             if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
-            if (limit >= 0 && use + L.types[k].vcpu * 1000 > limit) continue;
+            if (!limit_ok(L, k, use, limit, usem, limitm)) continue;
             const double carbon = L.types[k].p_ref_w * ci_gpwh;
             for (int z = 0; z < L.Z; ++z) {
               if (!(zm >> z & 1u)) continue;
@@ -1027,7 +1128,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           if (now_ready) rdy |= 1u << slot;
           else next_ready = min(next_ready, t + delay);
 #pragma unroll
-          for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq) if (qq == q) puse[qq] += L.types[bk].vcpu * 1000;
+          for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+            if (qq == q) puse[qq] += L.types[bk].vcpu * 1000;
           if (bc == 0) nsp++; else nod++;
           burn += bpr;
           launches++;
@@ -1069,7 +1171,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             long long pdb_pods = 0;
             int s_cpu = 0, s_mem = 0, s_pods = 0;
             uint32_t cm = 0, zm = 0;
-            int use = 0, limit = 0;
+            int use = 0, limit = 0, usem = 0;
+            const int limitm = w->pools[q].limit_mem_mi;
+            if (limitm >= 0) usem = pool_mem(q);
 #pragma unroll
             for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
               if (qq == q) { cm = pcm[qq]; zm = pzm[qq]; use = puse[qq]; limit = plimit[qq]; }
@@ -1088,7 +1192,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             cand &= ~(1u << best);
             if (pdb_pods > allowed || !cm) continue;
             int bk, bz, bc, bpr;
-            find_offer(zm, cm, use, limit, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
+            find_offer(zm, cm, use, limit, usem, limitm, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
             if (bk < 0 || bpr >= bprice) continue;
             launch_replacement(q, slot, best, bk, bz, bc, bpr);
             deleted++;
@@ -1248,7 +1352,9 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               // or an offering they are evicted and the node goes now
               int s_cpu = 0, s_mem = 0, s_pods = 0;
               uint32_t cm = 0, zm = 0;
-              int use = 0, limit = 0;
+              int use = 0, limit = 0, usem = 0;
+              const int limitm = w->pools[q].limit_mem_mi;
+              if (limitm >= 0) usem = pool_mem(q);
 #pragma unroll
               for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
                 if (qq == q) { cm = pcm[qq]; zm = pzm[qq]; use = puse[qq]; limit = plimit[qq]; }
@@ -1263,7 +1369,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               const uint32_t fr = ~used & slot_mask;
               int bk = -1, bz = 0, bc = 0, bpr = 0;
               // an ordinary provisioning decision: the F2 launch rule
-              if (s_pods > 0 && fr && cm) lane_launch(zm, cm, use, limit, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
+              if (s_pods > 0 && fr && cm)
+                lane_launch(zm, cm, use, limit, usem, limitm, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
               if (bk >= 0) {
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n)

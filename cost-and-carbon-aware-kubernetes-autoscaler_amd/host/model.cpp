@@ -145,6 +145,7 @@ Tables builtin_tables(const std::string& which, double ci, uint64_t seed) {
       t.idle_nw = std::llround(p_idle * 1e9);
       t.dyn_nw_per_m = std::llround(p_dyn * 1e9 / (double)t.alloc_cpu_m);
       t.p_ref_w = p_idle + 0.5 * p_dyn;
+      t.mem_mi = (int32_t)mem_mi;
       T.types.push_back(t);
       od.push_back(fams[f].uph * v / 2);
     }
@@ -257,7 +258,8 @@ static ccka_hpa_rules rules_from(const Value* b, bool up, int default_stab) {
   if (const Value* ps = b->get("policies"); ps && ps->is_seq()) {
     r.n_policies = 0;
     for (auto& p : ps->seq) {
-      if (r.n_policies == 2) throw ParseError("HPA behavior: more than 2 policies per direction");
+      if (r.n_policies == CCKA_HPA_MAX_POLICIES)
+        throw ParseError("HPA behavior: more than " + std::to_string(CCKA_HPA_MAX_POLICIES) + " policies per direction");
       const std::string ty = p.get("type") ? p.get("type")->as_string() : "";
       r.policies[r.n_policies].type = ty == "Pods" ? CCKA_HPA_PODS : CCKA_HPA_PERCENT;
       r.policies[r.n_policies].value = (int32_t)(p.get("value") ? p.get("value")->as_int() : 0);
@@ -304,7 +306,13 @@ WorldMeta build_world(const ManifestStore& store, const PolicyEnv& env, const Ta
     meta.pool_strategy.push_back(sl ? sl->as_string() : "");
     ccka_pool& P = w->pools[q];
     P.limit_cpu_m = -1;
+    P.limit_mem_mi = -1;
     if (const Value* l = np.at({"spec", "limits", "cpu"})) P.limit_cpu_m = (int32_t)cpu_millis(l->as_string());
+    if (const Value* l = np.at({"spec", "limits", "memory"})) {
+      const int64_t m = mem_mib(l->as_string());
+      if (m < 0 || m > 0x7fffffff) throw ParseError("NodePool " + name + ": limits.memory out of range");
+      P.limit_mem_mi = (int32_t)m;
+    }
     P.budget_pct = 10;
     if (const Value* b = np.at({"spec", "disruption", "budgets", "0", "nodes"})) {
       const std::string s = b->as_string();

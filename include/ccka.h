@@ -39,7 +39,11 @@ extern "C" {
 #define CCKA_MAX_POOLS 4
 #define CCKA_MAX_DEPLOY 16
 #define CCKA_MAX_NODES 16
-#define CCKA_HIST 8              /* history ring depth (steps) for HPA windows */
+#define CCKA_HIST 8              /* register history ring depth (decisions) of the fast paths */
+#define CCKA_HPA_MAX_POLICIES 4   /* scaling policies per direction */
+#define CCKA_HPA_MAX_WINDOW_S 3600 /* stabilizationWindowSeconds upper bound (autoscaling/v2) */
+#define CCKA_HPA_MAX_PERIOD_S 1800 /* policy periodSeconds upper bound (autoscaling/v2) */
+#define CCKA_HPA_HIST_MAX 360     /* decision history entries: 3600 s / the shortest sync (10 s) */
 #define CCKA_HOURS 24
 
 enum ccka_status {
@@ -83,7 +87,8 @@ typedef struct ccka_itype {
   int64_t idle_nw;        /* llround(vcpu*Wmin*PUE * 1e9)                      */
   int64_t dyn_nw_per_m;   /* llround(vcpu*(Wmax-Wmin)*PUE * 1e9 / alloc_cpu_m) */
   double p_ref_w;         /* p_idle + 0.5*p_dyn in W (launch-score power)      */
-  double _reserved;
+  int32_t mem_mi;         /* memory capacity MiB (NodePool spec.limits.memory) */
+  int32_t _pad;
 } ccka_itype;
 
 /* A NodePool patch profile (merge semantics: 0 / -1 = keep). */
@@ -99,20 +104,22 @@ typedef struct ccka_pool {
   int32_t budget_pct;           /* disruption budget nodes %, default 10  */
   ccka_pool_patch base;         /* the NodePool as created                */
   ccka_pool_patch profile[3];   /* RESET, OFFPEAK, PEAK                   */
+  int32_t limit_mem_mi;         /* spec.limits.memory in MiB, -1 none     */
+  int32_t _pad;
 } ccka_pool;
 
 typedef struct ccka_hpa_policy {
   int32_t type;       /* CCKA_HPA_PODS / CCKA_HPA_PERCENT */
   int32_t value;
-  int32_t period_s;   /* <= 480 */
+  int32_t period_s;   /* 1..CCKA_HPA_MAX_PERIOD_S */
 } ccka_hpa_policy;
 
 typedef struct ccka_hpa_rules {
   int32_t select;       /* CCKA_SELECT_* */
-  int32_t n_policies;   /* 0..2 */
-  int32_t stab_window_s;/* <= 480 */
+  int32_t n_policies;   /* 0..CCKA_HPA_MAX_POLICIES */
+  int32_t stab_window_s;/* 0..CCKA_HPA_MAX_WINDOW_S */
   int32_t _pad;
-  ccka_hpa_policy policies[2];
+  ccka_hpa_policy policies[CCKA_HPA_MAX_POLICIES];
 } ccka_hpa_rules;
 
 typedef struct ccka_deployment {
@@ -170,6 +177,12 @@ typedef struct ccka_world {
   int32_t disrupt_ext;          /* CCKA_DISRUPT_* bits: Karpenter disruption
                                    beyond WhenEmpty / WhenEmptyOrUnderutilized
                                    deletes (SEMANTICS 3.G0, 3.G2) */
+  int32_t hpa_sync_s;           /* HPA / KEDA decision period (kube-controller-manager
+                                   --horizontal-pod-autoscaler-sync-period): 0 or 60 =
+                                   one decision per 60-s step; 10, 15, 20, 30 = 60/s
+                                   decisions per step on the step's metric sample
+                                   (SEMANTICS 3.C) */
+  int32_t _pad2;
 } ccka_world;
 
 /* Per-scenario parameters, SoA, host pointers. NULL ⇒ world default. */

@@ -26,6 +26,7 @@
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
+#include <stddef.h>
 #include <string.h>
 
 #define O_BIG 0x3fffffffffffffffLL
@@ -126,18 +127,29 @@ int32_t ccka_oracle_keda_proposal(int32_t cur, int64_t metric, int64_t threshold
   return (int32_t)ceil((double)metric / (double)threshold);
 }
 
-static int32_t o_rate_up(int32_t cur, const ccka_hpa_rules* up, const int32_t* deltas) {
+/* history entry k holds the decision (k + 1) * sync_s seconds ago; a record
+ * counts inside a window / period W iff its age < W (upstream's
+ * timestamp.Add(W).After(now)) */
+static int o_entries(int32_t window_s, int32_t sync_s) { return window_s > sync_s ? (window_s - 1) / sync_s : 0; }
+
+/* replicas changed by the scaler within a policy period: (added, deleted) */
+static void o_period_sums(const ccka_hpa_policy* p, int32_t sync_s, const int32_t* deltas, int n, int64_t* added,
+                          int64_t* deleted) {
+  *added = *deleted = 0;
+  const int m = o_entries(p->period_s, sync_s) < n ? o_entries(p->period_s, sync_s) : n;
+  for (int k = 0; k < m; ++k) {
+    if (deltas[k] > 0) *added += deltas[k];
+    if (deltas[k] < 0) *deleted += -deltas[k];
+  }
+}
+
+static int32_t o_rate_up(int32_t cur, const ccka_hpa_rules* up, int32_t sync_s, const int32_t* deltas, int n) {
   if (up->select == CCKA_SELECT_DISABLED) return cur;
   int64_t res = up->select == CCKA_SELECT_MIN ? INT32_MAX : INT32_MIN;
   for (int i = 0; i < up->n_policies; ++i) {
     const ccka_hpa_policy* p = &up->policies[i];
-    int64_t added = 0, deleted = 0;
-    for (int k = 0; k < CCKA_HIST; ++k) {
-      if ((k + 1) * CCKA_STEP_SECONDS < p->period_s) {
-        if (deltas[k] > 0) added += deltas[k];
-        if (deltas[k] < 0) deleted += -deltas[k];
-      }
-    }
+    int64_t added, deleted;
+    o_period_sums(p, sync_s, deltas, n, &added, &deleted);
     const int64_t ps = cur - added + deleted;
     int64_t prop;
     if (p->type == CCKA_HPA_PODS) prop = ps + p->value;
@@ -148,19 +160,14 @@ static int32_t o_rate_up(int32_t cur, const ccka_hpa_rules* up, const int32_t* d
   return (int32_t)res;
 }
 
-static int32_t o_rate_down(int32_t cur, const ccka_hpa_rules* dn, const int32_t* deltas) {
+static int32_t o_rate_down(int32_t cur, const ccka_hpa_rules* dn, int32_t sync_s, const int32_t* deltas, int n) {
   if (dn->select == CCKA_SELECT_DISABLED) return cur;
   /* Max selects the policy allowing the biggest change: the minimum count */
   int64_t res = dn->select == CCKA_SELECT_MIN ? INT32_MIN : INT32_MAX;
   for (int i = 0; i < dn->n_policies; ++i) {
     const ccka_hpa_policy* p = &dn->policies[i];
-    int64_t added = 0, deleted = 0;
-    for (int k = 0; k < CCKA_HIST; ++k) {
-      if ((k + 1) * CCKA_STEP_SECONDS < p->period_s) {
-        if (deltas[k] > 0) added += deltas[k];
-        if (deltas[k] < 0) deleted += -deltas[k];
-      }
-    }
+    int64_t added, deleted;
+    o_period_sums(p, sync_s, deltas, n, &added, &deleted);
     const int64_t ps = cur - added + deleted;
     int64_t prop;
     if (p->type == CCKA_HPA_PODS) prop = ps - p->value;
@@ -171,17 +178,17 @@ static int32_t o_rate_down(int32_t cur, const ccka_hpa_rules* dn, const int32_t*
   return (int32_t)res;
 }
 
-int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, int32_t max_r,
-                                 const ccka_hpa_rules* up, const ccka_hpa_rules* down,
-                                 const int32_t* recs, const uint8_t* rec_valid,
-                                 const int32_t* deltas) {
+int32_t ccka_oracle_hpa_behavior_n(int32_t cur, int32_t proposal, int32_t min_r, int32_t max_r,
+                                   const ccka_hpa_rules* up, const ccka_hpa_rules* down, int32_t sync_s,
+                                   const int32_t* recs, const uint8_t* rec_valid, const int32_t* deltas, int32_t n) {
   /* stabilizeRecommendationWithBehaviors */
   int32_t upr = proposal, dnr = proposal;
-  for (int k = 0; k < CCKA_HIST; ++k) {
+  const int nu = o_entries(up->stab_window_s, sync_s), nd = o_entries(down->stab_window_s, sync_s);
+  const int m = (nu > nd ? nu : nd) < n ? (nu > nd ? nu : nd) : n;
+  for (int k = 0; k < m; ++k) {
     if (!rec_valid[k]) continue;
-    const int age = (k + 1) * CCKA_STEP_SECONDS;
-    if (age < up->stab_window_s && recs[k] < upr) upr = recs[k];
-    if (age < down->stab_window_s && recs[k] > dnr) dnr = recs[k];
+    if (k < nu && recs[k] < upr) upr = recs[k];
+    if (k < nd && recs[k] > dnr) dnr = recs[k];
   }
   int32_t rec = cur;
   if (rec < upr) rec = upr;
@@ -189,17 +196,25 @@ int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, i
   /* convertDesiredReplicasWithBehaviorRate */
   int32_t lo = min_r, hi = max_r;
   if (rec > cur) {
-    int32_t lim = o_rate_up(cur, up, deltas);
+    int32_t lim = o_rate_up(cur, up, sync_s, deltas, n);
     if (lim < cur) lim = cur;
     if (hi > lim) hi = lim;
   } else if (rec < cur) {
-    int32_t lim = o_rate_down(cur, down, deltas);
+    int32_t lim = o_rate_down(cur, down, sync_s, deltas, n);
     if (lim > cur) lim = cur;
     if (lo < lim) lo = lim;
   }
   if (rec < lo) return lo;
   if (rec > hi) return hi;
   return rec;
+}
+
+int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, int32_t max_r,
+                                 const ccka_hpa_rules* up, const ccka_hpa_rules* down,
+                                 const int32_t* recs, const uint8_t* rec_valid,
+                                 const int32_t* deltas) {
+  return ccka_oracle_hpa_behavior_n(cur, proposal, min_r, max_r, up, down, CCKA_STEP_SECONDS, recs, rec_valid, deltas,
+                                    CCKA_HIST);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -218,9 +233,10 @@ typedef struct {
 
 typedef struct {
   int replicas;
-  int32_t rec[CCKA_HIST];
-  uint8_t rec_valid[CCKA_HIST];
-  int32_t delta[CCKA_HIST];
+  int32_t rec[CCKA_HPA_HIST_MAX]; /* entry k: the decision (k + 1) * sync_s ago */
+  uint8_t rec_valid[CCKA_HPA_HIST_MAX];
+  int32_t delta[CCKA_HPA_HIST_MAX];
+  int hn; /* entries any window or period of this deployment reaches */
   int last_active;
 } o_dep;
 
@@ -287,11 +303,24 @@ static int64_t o_node_fit(const o_env* e, const o_node* nd, int d) {
   return f < 0 ? 0 : f;
 }
 
-/* type candidate for a claim: holds sums, limit, offered in masks */
+/* resources of a pool's nodes: CPU capacity (millicores) and memory capacity (MiB) */
+typedef struct {
+  int64_t cpu, mem;
+} o_use;
+
+/* NodePool spec.limits: a new node of type ty keeps the pool within its CPU
+ * and memory limits (SEMANTICS 3.F) */
+static int o_limits_ok(const ccka_pool* pl, o_use u, const ccka_itype* ty) {
+  if (pl->limit_cpu_m >= 0 && u.cpu + (int64_t)ty->vcpu * 1000 > pl->limit_cpu_m) return 0;
+  if (pl->limit_mem_mi >= 0 && u.mem + (int64_t)ty->mem_mi > pl->limit_mem_mi) return 0;
+  return 1;
+}
+
+/* type candidate for a claim: holds sums, limits, offered in masks */
 static int o_type_ok(const o_env* e, int r, int h, int k, uint32_t zm, uint32_t cm,
-                     int64_t pool_use, int32_t limit) {
+                     o_use pool_use, const ccka_pool* pl) {
   const ccka_itype* ty = &e->w->types[k];
-  if (limit >= 0 && pool_use + (int64_t)ty->vcpu * 1000 > limit) return 0;
+  if (!o_limits_ok(pl, pool_use, ty)) return 0;
   for (int z = 0; z < e->Z; ++z) {
     if (!(zm >> z & 1u)) continue;
     for (int c = 0; c < 2; ++c)
@@ -301,10 +330,10 @@ static int o_type_ok(const o_env* e, int r, int h, int k, uint32_t zm, uint32_t 
 }
 
 static int64_t o_claim_j(const o_env* e, int r, int h, const o_claim* cl, uint32_t cm, int d,
-                         int64_t pool_use, int32_t limit) {
+                         o_use pool_use, const ccka_pool* pl) {
   int64_t best = 0;
   for (int k = 0; k < e->K; ++k) {
-    if (!o_type_ok(e, r, h, k, cl->zone, cm, pool_use, limit)) continue;
+    if (!o_type_ok(e, r, h, k, cl->zone, cm, pool_use, pl)) continue;
     const ccka_itype* ty = &e->w->types[k];
     const int64_t f = o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, cl->s_cpu, cl->s_mem,
                             cl->s_pods, e->w->deploy[d].req_cpu_m, e->w->deploy[d].req_mem_mi);
@@ -315,7 +344,6 @@ static int64_t o_claim_j(const o_env* e, int r, int h, const o_claim* cl, uint32
 
 typedef struct {
   o_pool pools[CCKA_MAX_POOLS];
-  o_dep dep[CCKA_MAX_DEPLOY];
   o_node nodes[CCKA_MAX_NODES];
   int profile;
   int64_t cost, pend_min;
@@ -324,6 +352,7 @@ typedef struct {
   int slo, nmin_spot, nmin_od, launches, deletions, peak_nodes;
   uint32_t last_choice, hash;
   int pool_launches[CCKA_MAX_POOLS];
+  o_dep dep[CCKA_MAX_DEPLOY]; /* last: only the first D are initialised */
 } o_state;
 
 /* Karpenter drift: the node's zone or capacity type no longer satisfies its
@@ -337,13 +366,13 @@ static void o_free(o_node* nodes, int NN, int n) {
 
 /* cheapest single offering (price, k, z, c) holding the sums under zone mask
  * zm, capacity mask cm and the pool CPU limit; -1 if none (SEMANTICS 3.G2) */
-static int o_offer(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, int64_t use, int32_t limit,
+static int o_offer(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, o_use use, const ccka_pool* pl,
                    int64_t sc, int64_t sm, int64_t sp, int* bz, int* bc, int32_t* bp) {
   int bk = -1;
   for (int k = 0; k < e->K; ++k) {
     const ccka_itype* ty = &e->w->types[k];
     if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, sc, sm, sp, 0, 0) < 0) continue;
-    if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+    if (!o_limits_ok(pl, use, ty)) continue;
     for (int z = 0; z < e->Z; ++z) {
       if (!(zm >> z & 1u)) continue;
       for (int cc = 0; cc < 2; ++cc) {
@@ -361,7 +390,7 @@ static int o_offer(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, int64
  * z in zm, c in cm, price > 0; if spot is allowed and any spot offering is
  * feasible only spot offerings compete; the lexicographic minimum of
  * (score, k, z, c), score = price + carbon_weight*1000*(p_ref_w*ci). -1 if none. */
-static int o_launch_choice(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, int64_t use, int32_t limit,
+static int o_launch_choice(const o_env* e, int r, int h, uint32_t zm, uint32_t cm, o_use use, const ccka_pool* pl,
                            int64_t sc, int64_t sm, int64_t sp, double wc1000, int* bz, int* bc, int32_t* bp) {
   const ccka_world* w = e->w;
   int spot_only = 0;
@@ -369,7 +398,7 @@ static int o_launch_choice(const o_env* e, int r, int h, uint32_t zm, uint32_t c
     for (int k = 0; k < e->K && !spot_only; ++k) {
       const ccka_itype* ty = &w->types[k];
       if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, sc, sm, sp, 0, 0) < 0) continue;
-      if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+      if (!o_limits_ok(pl, use, ty)) continue;
       for (int z = 0; z < e->Z; ++z)
         if ((zm >> z & 1u) && o_price(e, r, h, k, z, 0) > 0) { spot_only = 1; break; }
     }
@@ -379,7 +408,7 @@ static int o_launch_choice(const o_env* e, int r, int h, uint32_t zm, uint32_t c
   for (int k = 0; k < e->K; ++k) {
     const ccka_itype* ty = &w->types[k];
     if (o_fit(ty->alloc_cpu_m, ty->alloc_mem_mi, ty->max_pods, sc, sm, sp, 0, 0) < 0) continue;
-    if (limit >= 0 && use + (int64_t)ty->vcpu * 1000 > limit) continue;
+    if (!o_limits_ok(pl, use, ty)) continue;
     for (int z = 0; z < e->Z; ++z) {
       if (!(zm >> z & 1u)) continue;
       for (int cc = 0; cc < 2; ++cc) {
@@ -424,6 +453,16 @@ static int o_tainted(const o_node* nodes, int NN, int n) {
   return 0;
 }
 
+static o_use o_pool_use(const o_state* st, const ccka_world* w, int NN, int p) {
+  o_use u = {0, 0};
+  for (int m = 0; m < NN; ++m)
+    if (st->nodes[m].used && st->nodes[m].pool == p) {
+      u.cpu += (int64_t)w->types[st->nodes[m].type].vcpu * 1000;
+      u.mem += w->types[st->nodes[m].type].mem_mi;
+    }
+  return u;
+}
+
 static int o_drifted(const o_state* st, const o_node* nd) {
   const o_pool* pl = &st->pools[nd->pool];
   return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
@@ -436,7 +475,11 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
   const ccka_world* w = e->w;
   const int D = e->D, NN = e->N;
   o_state st;
-  memset(&st, 0, sizeof st);
+  memset(&st, 0, offsetof(o_state, dep));
+  memset(st.dep, 0, (size_t)D * sizeof(o_dep));
+  /* HPA / KEDA decisions per step (SEMANTICS 3.C sub-steps) */
+  const int32_t sync_s = w->hpa_sync_s > 0 ? w->hpa_sync_s : CCKA_STEP_SECONDS;
+  const int nsub = CCKA_STEP_SECONDS / sync_s;
   /* load column: the scenario's own trace, or its shared trace (policy sweeps) */
   const int64_t nl = sc->n_traces > 0 ? sc->n_traces : nsc;
   const int64_t col = sc->n_traces > 0 ? (sc->first_id + i) % sc->n_traces : i;
@@ -461,6 +504,14 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     }
     st.dep[d].replicas = dp->replicas0;
     st.dep[d].last_active = 0;
+    int hn = o_entries(dp->up.stab_window_s, sync_s);
+    const int hd = o_entries(downr[d].stab_window_s, sync_s);
+    if (hd > hn) hn = hd;
+    for (int q = 0; q < dp->up.n_policies; ++q)
+      if (o_entries(dp->up.policies[q].period_s, sync_s) > hn) hn = o_entries(dp->up.policies[q].period_s, sync_s);
+    for (int q = 0; q < dp->down.n_policies; ++q)
+      if (o_entries(dp->down.policies[q].period_s, sync_s) > hn) hn = o_entries(dp->down.policies[q].period_s, sync_s);
+    st.dep[d].hn = hn < CCKA_HPA_HIST_MAX ? hn : CCKA_HPA_HIST_MAX;
   }
   for (int p = 0; p < w->n_pools; ++p) {
     memset(&st.pools[p], 0, sizeof(o_pool));
@@ -508,9 +559,10 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       for (int p = 0; p < w->n_pools; ++p) o_patch(&st.pools[p], &w->pools[p].profile[prof]);
       st.profile = prof;
     }
-    /* ---- C. scalers ---- */
+    /* ---- C. scalers: nsub decisions on the step's metric sample ---- */
     int util_valid[CCKA_MAX_DEPLOY], util[CCKA_MAX_DEPLOY], keda_act[CCKA_MAX_DEPLOY] = {0};
     int64_t Lt[CCKA_MAX_DEPLOY];
+    for (int sub = 0; sub < nsub; ++sub)
     for (int d = 0; d < D; ++d) {
       const ccka_deployment* dp = &w->deploy[d];
       o_dep* ds = &st.dep[d];
@@ -540,8 +592,8 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
                                                        dp->tolerance, &u);
           util_valid[d] = 1;
           util[d] = u;
-          desired = ccka_oracle_hpa_behavior(cur, proposal, minr, mx, &dp->up, &downr[d], ds->rec,
-                                             ds->rec_valid, ds->delta);
+          desired = ccka_oracle_hpa_behavior_n(cur, proposal, minr, mx, &dp->up, &downr[d], sync_s, ds->rec,
+                                               ds->rec_valid, ds->delta, ds->hn);
           ran = 1;
         }
       } else if (dp->scaler == CCKA_SCALER_KEDA) {
@@ -572,22 +624,24 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
                                                            w->deploy[d + j].keda_threshold, dp->tolerance);
               if (pj > proposal) proposal = pj;
             }
-            desired = ccka_oracle_hpa_behavior(cur, proposal, minr, mx, &dp->up, &dp->down, ds->rec,
-                                               ds->rec_valid, ds->delta);
+            desired = ccka_oracle_hpa_behavior_n(cur, proposal, minr, mx, &dp->up, &dp->down, sync_s, ds->rec,
+                                                 ds->rec_valid, ds->delta, ds->hn);
             ran = 1;
           }
         }
       }
       if (dp->scaler == CCKA_SCALER_HPA || dp->scaler == CCKA_SCALER_KEDA) {
-        /* shift history rings: entry 0 becomes this step */
-        for (int k = CCKA_HIST - 1; k > 0; --k) {
-          ds->rec[k] = ds->rec[k - 1];
-          ds->rec_valid[k] = ds->rec_valid[k - 1];
-          ds->delta[k] = ds->delta[k - 1];
+        /* shift the history: entry 0 becomes this decision */
+        if (ds->hn > 0) {
+          for (int k = ds->hn - 1; k > 0; --k) {
+            ds->rec[k] = ds->rec[k - 1];
+            ds->rec_valid[k] = ds->rec_valid[k - 1];
+            ds->delta[k] = ds->delta[k - 1];
+          }
+          ds->rec[0] = ran ? proposal : 0;
+          ds->rec_valid[0] = (uint8_t)ran;
+          ds->delta[0] = (hpa_path && desired != cur) ? desired - cur : 0;
         }
-        ds->rec[0] = ran ? proposal : 0;
-        ds->rec_valid[0] = (uint8_t)ran;
-        ds->delta[0] = (hpa_path && desired != cur) ? desired - cur : 0;
         ds->replicas = desired;
       }
     }
@@ -633,12 +687,15 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     }
     /* ---- F2. provisioning ---- */
     {
-      int64_t pool_use[CCKA_MAX_POOLS];
-      for (int p = 0; p < w->n_pools; ++p) pool_use[p] = 0;
+      o_use pool_use[CCKA_MAX_POOLS];
+      memset(pool_use, 0, sizeof pool_use);
       int slot_taken[CCKA_MAX_NODES];
       for (int n = 0; n < NN; ++n) {
         slot_taken[n] = st.nodes[n].used;
-        if (st.nodes[n].used) pool_use[st.nodes[n].pool] += (int64_t)w->types[st.nodes[n].type].vcpu * 1000;
+        if (st.nodes[n].used) {
+          pool_use[st.nodes[n].pool].cpu += (int64_t)w->types[st.nodes[n].type].vcpu * 1000;
+          pool_use[st.nodes[n].pool].mem += w->types[st.nodes[n].type].mem_mi;
+        }
       }
       o_claim claims[CCKA_MAX_NODES];
       int ncl = 0;
@@ -651,7 +708,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           o_claim* cl = &claims[c];
           const uint32_t cm = cl->cap & capsel[d];
           if (!cm) continue;
-          const int64_t j = o_claim_j(e, r, h, cl, cm, d, pool_use[cl->pool], w->pools[cl->pool].limit_cpu_m);
+          const int64_t j = o_claim_j(e, r, h, cl, cm, d, pool_use[cl->pool], &w->pools[cl->pool]);
           if (j <= 0) continue;
           const int k = (int)(j < rem ? j : rem);
           cl->cap = cm;
@@ -675,7 +732,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
             nc.pool = p;
             nc.cap = cm;
             nc.zone = st.pools[p].zone_mask;
-            const int64_t j = o_claim_j(e, r, h, &nc, cm, d, pool_use[p], w->pools[p].limit_cpu_m);
+            const int64_t j = o_claim_j(e, r, h, &nc, cm, d, pool_use[p], &w->pools[p]);
             if (j > 0) { chosen = p; jj = j; break; }
           }
           if (chosen < 0) break;
@@ -696,10 +753,9 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       /* launch in creation order */
       for (int c = 0; c < ncl; ++c) {
         o_claim* cl = &claims[c];
-        const int32_t limit = w->pools[cl->pool].limit_cpu_m;
         int bz = 0, bc = 0;
         int32_t bpr = 0;
-        const int bk = o_launch_choice(e, r, h, cl->zone, cl->cap, pool_use[cl->pool], limit, cl->s_cpu, cl->s_mem,
+        const int bk = o_launch_choice(e, r, h, cl->zone, cl->cap, pool_use[cl->pool], &w->pools[cl->pool], cl->s_cpu, cl->s_mem,
                                        cl->s_pods, wc1000, &bz, &bc, &bpr);
         if (bk < 0) { continue; /* dropped: slot stays free */ }
         o_node* nd = &st.nodes[cl->slot];
@@ -712,7 +768,8 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
         nd->ready_step = t + w->provision_delay_steps;
         nd->last_event = t;
         for (int d = 0; d < D; ++d) nd->pods[d] = cl->pods[d];
-        pool_use[cl->pool] += (int64_t)w->types[bk].vcpu * 1000;
+        pool_use[cl->pool].cpu += (int64_t)w->types[bk].vcpu * 1000;
+        pool_use[cl->pool].mem += w->types[bk].mem_mi;
         st.launches++;
         st.pool_launches[cl->pool]++;
         st.last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)cl->pool << 16;
@@ -794,7 +851,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
            * requirements takes them when ready (G1); without a free slot or
            * an offering they are evicted and the node goes now */
           {
-            int64_t sc = 0, sm = 0, sp = 0, use = 0;
+            int64_t sc = 0, sm = 0, sp = 0;
             uint32_t cm = st.pools[p].cap_mask;
             for (int d = 0; d < D; ++d) {
               if (left[d] <= 0) continue;
@@ -805,12 +862,11 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
             }
             int slot = -1;
             for (int m = 0; m < NN; ++m) if (!st.nodes[m].used) { slot = m; break; }
-            for (int m = 0; m < NN; ++m)
-              if (st.nodes[m].used && st.nodes[m].pool == p) use += (int64_t)w->types[st.nodes[m].type].vcpu * 1000;
+            const o_use use = o_pool_use(&st, w, NN, p);
             int bz = 0, bc = 0, bk = -1;
             int32_t bp = 0;
             if (sp > 0 && slot >= 0 && cm)  /* an ordinary provisioning decision: the F2 rule */
-              bk = o_launch_choice(e, r, h, st.pools[p].zone_mask, cm, use, w->pools[p].limit_cpu_m, sc, sm, sp,
+              bk = o_launch_choice(e, r, h, st.pools[p].zone_mask, cm, use, &w->pools[p], sc, sm, sp,
                                    wc1000, &bz, &bc, &bp);
             if (bk >= 0) {
               for (int d = 0; d < D; ++d) dn->pods[d] = left[d];
@@ -913,13 +969,10 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
             s_pods += cn->pods[d];
           }
           if (pdb_pods > allowed || !cm) { rej2[best] = 1; continue; }
-          int64_t use = 0;
-          for (int n = 0; n < NN; ++n)
-            if (st.nodes[n].used && st.nodes[n].pool == p) use += (int64_t)w->types[st.nodes[n].type].vcpu * 1000;
-          const int32_t limit = w->pools[p].limit_cpu_m;
+          const o_use use = o_pool_use(&st, w, NN, p);
           int bz = 0, bc = 0;
           int32_t bp = 0;
-          const int bk = o_offer(e, r, h, st.pools[p].zone_mask, cm, use, limit, s_cpu, s_mem, s_pods, &bz, &bc, &bp);
+          const int bk = o_offer(e, r, h, st.pools[p].zone_mask, cm, use, &w->pools[p], s_cpu, s_mem, s_pods, &bz, &bc, &bp);
           if (bk < 0 || bp >= bprice) { rej2[best] = 1; continue; }
           o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, best);
           step_last_type = (uint16_t)bk;

@@ -46,6 +46,13 @@ int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, i
                                  const int32_t* recs, const uint8_t* rec_valid,
                                  const int32_t* deltas);
 
+/* The same with a decision history of n entries, entry k = the decision
+ * (k + 1) * sync_s seconds ago (windows up to CCKA_HPA_MAX_WINDOW_S, up to
+ * CCKA_HPA_MAX_POLICIES policies per direction). */
+int32_t ccka_oracle_hpa_behavior_n(int32_t cur, int32_t proposal, int32_t min_r, int32_t max_r,
+                                   const ccka_hpa_rules* up, const ccka_hpa_rules* down, int32_t sync_s,
+                                   const int32_t* recs, const uint8_t* rec_valid, const int32_t* deltas, int32_t n);
+
 /* Synthetic traces (SEMANTICS §4): out is [T][D][n]. */
 void ccka_oracle_sin_table(int32_t* out1440);
 void ccka_oracle_gen_load(const ccka_trace_gen* g, int32_t T, int32_t D, int64_t n,

@@ -64,6 +64,11 @@ def lib():
                                                C.POINTER(abi.HpaRules), C.POINTER(abi.HpaRules),
                                                C.POINTER(C.c_int32), C.POINTER(C.c_uint8),
                                                C.POINTER(C.c_int32)]
+        L.ccka_oracle_hpa_behavior_n.restype = C.c_int32
+        L.ccka_oracle_hpa_behavior_n.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                                 C.POINTER(abi.HpaRules), C.POINTER(abi.HpaRules), C.c_int32,
+                                                 C.POINTER(C.c_int32), C.POINTER(C.c_uint8),
+                                                 C.POINTER(C.c_int32), C.c_int32]
         L.ccka_oracle_sin_table.argtypes = [C.POINTER(C.c_int32)]
         L.ccka_oracle_gen_load.argtypes = [C.POINTER(abi.TraceGen), C.c_int32, C.c_int32,
                                            C.c_int64, C.c_int64, C.POINTER(C.c_int32)]

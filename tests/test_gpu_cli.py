@@ -17,15 +17,15 @@ from parity import INT_FIELDS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("load_m,catalog,drift", [(100, "tiny", 0), (450, "small", 0), (450, "small", 1),
-                                                            (450, "small", 3)])
-def test_cli_replay_matches_oracle(tmp_path, load_m, catalog, drift):
+@pytest.mark.parametrize("load_m,catalog,drift,sync", [(100, "tiny", 0, 0), (450, "small", 0, 0), (450, "small", 1, 0),
+                                                        (450, "small", 3, 0), (450, "small", 1, 15)])
+def test_cli_replay_matches_oracle(tmp_path, load_m, catalog, drift, sync):
     out = tmp_path / "r.json"
     env = {k: v for k, v in os.environ.items() if k not in ("COUNT", "REPLICAS", "NP_SPOT", "NP_OD")}
     prom = tmp_path / "r.prom"
     txt = subprocess.run([CLI, "replay", "--catalog", catalog, "--load-m", str(load_m), "--json", str(out),
                           "--prom", str(prom)] + (["--drift"] if drift & 1 else [])
-                         + (["--replace"] if drift & 2 else []),
+                         + (["--replace"] if drift & 2 else []) + (["--hpa-sync", str(sync)] if sync else []),
                          env=env, check=True, capture_output=True, text=True, timeout=120).stdout
     assert "cost=$" in txt and "spot-preferred" in txt
     got = json.load(open(out))
@@ -38,6 +38,7 @@ def test_cli_replay_matches_oracle(tmp_path, load_m, catalog, drift):
     h.label("NodePool", "on-demand-slo", "autoscale.strategy=slo carbon.simulated=medium")
     w = h.build_world(catalog, 1440, 16)
     w.disrupt_ext = drift
+    w.hpa_sync_s = sync
     load = np.full((1440, 12, 1), load_m, np.int32)
     want, traj, det = po.rollout_world(w, ScenarioSet(1), load, traj=True, detail=True)
     for f in INT_FIELDS:
