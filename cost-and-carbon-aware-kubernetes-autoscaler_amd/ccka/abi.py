@@ -25,7 +25,7 @@ HPA_HIST_MAX = 360
 CAP_SPOT, CAP_OD = 1, 2
 POLICY_KEEP, WHEN_EMPTY, WHEN_EMPTY_OR_UNDERUTILIZED = 0, 1, 2
 SCALER_STATIC, SCALER_HPA, SCALER_KEDA, SCALER_KEDA_TRIGGER = 0, 1, 2, 3
-DISRUPT_DRIFT, DISRUPT_REPLACE = 1, 2
+DISRUPT_DRIFT, DISRUPT_REPLACE, DISRUPT_MULTI = 1, 2, 4
 PROFILE_RESET, PROFILE_OFFPEAK, PROFILE_PEAK = 0, 1, 2
 SELECT_MAX, SELECT_MIN, SELECT_DISABLED = 0, 1, 2
 HPA_PODS, HPA_PERCENT = 1, 2

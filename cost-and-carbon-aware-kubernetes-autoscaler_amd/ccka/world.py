@@ -296,6 +296,7 @@ class WorldSpec:
     carbon_weight: float = 0.0
     drift: int = 0                 # CCKA_DISRUPT_DRIFT
     replace: int = 0               # CCKA_DISRUPT_REPLACE
+    multi: int = 0                 # CCKA_DISRUPT_MULTI
     hpa_sync_s: int = 0            # HPA decision period: 0/60 = once per step; 10/15/20/30 = sub-steps
     _keep: list = field(default_factory=list, repr=False)
 
@@ -342,7 +343,8 @@ class WorldSpec:
         w.peak_end_min = self.peak_end
         w.peak_switch = self.peak_switch
         w.reset_ca_s = self.reset_ca_s
-        w.disrupt_ext = (abi.DISRUPT_DRIFT if self.drift else 0) | (abi.DISRUPT_REPLACE if self.replace else 0)
+        w.disrupt_ext = ((abi.DISRUPT_DRIFT if self.drift else 0) | (abi.DISRUPT_REPLACE if self.replace else 0)
+                         | (abi.DISRUPT_MULTI if self.multi else 0))
         w.hpa_sync_s = self.hpa_sync_s
         return w
 

@@ -352,15 +352,17 @@ static bool d1_disrupt_inert(const ccka_ctx* c) {
     }
     if (switching && !same) return false;
   }
+  bool weou = false;
+  for (int q = 0; q < w.n_pools; ++q) {
+    weou |= w.pools[q].base.policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
+    for (int s = 0; s < 3; ++s) weou |= w.pools[q].profile[s].policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
+  }
   if (w.disrupt_ext & CCKA_DISRUPT_REPLACE) {
-    bool weou = false;
-    for (int q = 0; q < w.n_pools; ++q) {
-      weou |= w.pools[q].base.policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
-      for (int s = 0; s < 3; ++s) weou |= w.pools[q].profile[s].policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
-    }
     const uint32_t sel = c->sc_capsel_or ? c->sc_capsel_or : w.deploy[0].cap_sel;
     if (weou && (sel & CCKA_CAP_OD)) return false;
   }
+  // multi-node consolidation needs a WhenEmptyOrUnderutilized pool
+  if ((w.disrupt_ext & CCKA_DISRUPT_MULTI) && weou) return false;
   return true;
 }
 
@@ -517,7 +519,7 @@ int ccka_set_world(ccka_ctx* c, const ccka_world* w) {
   if (w->n_pools < 1 || w->n_pools > CCKA_MAX_POOLS) return fail(c, CCKA_EINVAL, "n_pools out of range");
   if (w->n_deploy < 1 || w->n_deploy > CCKA_MAX_DEPLOY) return fail(c, CCKA_EINVAL, "n_deploy out of range");
   if (!w->price_uph || !w->ci_gpwh || !w->ci_gpwmin) return fail(c, CCKA_EINVAL, "tiles missing");
-  if (w->disrupt_ext & ~(CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE))
+  if (w->disrupt_ext & ~(CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE | CCKA_DISRUPT_MULTI))
     return fail(c, CCKA_EINVAL, "unknown disrupt_ext bits");
   if (w->base_type < 0 || w->base_type >= w->n_types) return fail(c, CCKA_EINVAL, "base_type out of range");
   if (w->provision_delay_steps < 0 || w->start_minute < 0) return fail(c, CCKA_EINVAL, "negative timing");

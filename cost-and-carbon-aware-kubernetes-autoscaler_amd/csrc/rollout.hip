@@ -464,6 +464,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   const int pdb_pct = gw->pdb_min_available_pct;
   const bool gdrift = (gw->disrupt_ext & CCKA_DISRUPT_DRIFT) != 0;
   const bool greplace = (gw->disrupt_ext & CCKA_DISRUPT_REPLACE) != 0;
+  const bool gmulti = (gw->disrupt_ext & CCKA_DISRUPT_MULTI) != 0;
   const int slo_util = gw->slo_util_pct;
   const int base_nodes = gw->base_nodes, base_type = gw->base_type;
 
@@ -519,7 +520,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   // node slots; `used` / `rdy` are bitmasks over slots. nprice caches the
   // slot's offering price for the current hour, ncap (D == 1) its pod capacity.
   uint32_t ninfo[MAXN];
-  int nsrc[MAXN];  // replacement node: 1 + the slot it replaces (SEMANTICS 3.G2)
+  uint32_t nsrc[MAXN];  // replacement node: bit m = it replaces slot m (SEMANTICS 3.G2, 3.G3)
   int nready[MAXN], nlast[MAXN], nprice[MAXN], ncap[MAXN];
   int npods[MAXN][DMAX];
 #pragma unroll
@@ -533,7 +534,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     uint32_t m = 0;
 #pragma unroll
     for (int n = 0; n < MAXN; ++n)
-      if (nsrc[n]) m |= (1u << n) | (1u << (nsrc[n] - 1));
+      if (nsrc[n]) m |= (1u << n) | nsrc[n];
     return m;
   };
 
@@ -826,7 +827,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       // ---- E. kube-scheduler (ready) / F1. nomination (in-flight) ----
       // nodes tainted karpenter.sh/disrupted (a source whose pre-spun
       // replacement is in flight, and that replacement) take no other pods
-      const uint32_t tnt = (greplace || gdrift) ? taint_mask() : 0u;
+      const uint32_t tnt = (greplace || gdrift || gmulti) ? taint_mask() : 0u;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
         if (d >= D) break;
@@ -1036,7 +1037,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         // a freed slot's pending replacement becomes an ordinary node
         auto unlink = [&](int b) {
 #pragma unroll
-          for (int m = 0; m < MAXN; ++m) if (nsrc[m] == b + 1) nsrc[m] = 0;
+          for (int m = 0; m < MAXN; ++m) nsrc[m] &= ~(1u << b);
         };
         auto free_slot = [&](int b) {
 #pragma unroll
@@ -1108,8 +1109,8 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             }
           }
         };
-        // a pre-spun replacement node for slot `src` (no pods until it takes over)
-        auto launch_replacement = [&](int q, int slot, int src, int bk, int bz, int bc, int bpr) {
+        // a pre-spun replacement node for the slots in `srcm` (no pods until it takes over)
+        auto launch_replacement = [&](int q, int slot, uint32_t srcm, int bk, int bz, int bc, int bpr) {
           const bool now_ready = delay == 0;
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
@@ -1119,7 +1120,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               nlast[n] = t;
               nprice[n] = bpr;
               ncap[n] = DMAX == 1 ? L.cap1[bk] : 0;
-              nsrc[n] = src + 1;
+              nsrc[n] = srcm;
 #pragma unroll
               for (int e = 0; e < DMAX; ++e) npods[n][e] = 0;
             }
@@ -1147,7 +1148,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
           uint32_t srcm = 0, pq = 0;
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
-            if (nsrc[n]) srcm |= 1u << (nsrc[n] - 1);
+            srcm |= nsrc[n];
             pq |= (ni_pool(ninfo[n]) == q && ni_cap(ninfo[n]) == 1 ? 1u : 0u) << n;
           }
           uint32_t cand = rdy & pq & ~srcm;
@@ -1194,65 +1195,245 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             int bk, bz, bc, bpr;
             find_offer(zm, cm, use, limit, usem, limitm, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
             if (bk < 0 || bpr >= bprice) continue;
-            launch_replacement(q, slot, best, bk, bz, bc, bpr);
+            launch_replacement(q, slot, 1u << best, bk, bz, bc, bpr);
             deleted++;
             break;
           }
         };
-        // ---- G1. ready replacements take over their source's pods (SEMANTICS 3.G0, 3.G2) ----
-        if (greplace || gdrift) {
+        // ---- G3. multi-node consolidation (SEMANTICS 3.G3): Karpenter's firstN
+        // binary search over the prefix (>= 2 candidates, consolidation order)
+        // that can leave together with at most one strictly cheaper
+        // replacement; the winning prefix is re-evaluated with commit = true
+        // (one evaluation site keeps the unrolled slot loops emitted once)
+        auto try_multi = [&](int q, int qca, int budget, int& deleted) -> bool {
+          if (deleted >= budget) return false;
+          const uint32_t tn = taint_mask();
+          uint32_t cset = 0;
+          int cpods[MAXN];
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            int pods = 0;
+#pragma unroll
+            for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n][d] : 0;
+            cpods[n] = pods;
+            const bool c = ((rdy & ~tn) >> n & 1u) && ni_pool(ninfo[n]) == q &&
+                           (t - nlast[n]) * CCKA_STEP_SECONDS >= qca && pods > 0;
+            cset |= (c ? 1u : 0u) << n;
+          }
+          // rank in (pods asc, price desc, slot asc) order; ordl nibble r = slot of rank r
+          unsigned long long ordl = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            int rk = 0;
+#pragma unroll
+            for (int m = 0; m < MAXN; ++m) {
+              const bool before = cpods[m] < cpods[n] ||
+                                  (cpods[m] == cpods[n] && (nprice[m] > nprice[n] || (nprice[m] == nprice[n] && m < n)));
+              rk += ((cset >> m & 1u) && before) ? 1 : 0;
+            }
+            if (cset >> n & 1u) ordl |= (unsigned long long)n << (4 * rk);
+          }
+          const int nc = min(__popc(cset), budget - deleted);
+          int lo = 1, hi = nc - 1, bestk = 0, mid = 0;
+          bool acted = false;
+          while (true) {
+            int k;
+            bool commit = false;
+            if (lo <= hi) { mid = (lo + hi) / 2; k = mid + 1; }
+            else if (bestk) { k = bestk; commit = true; }
+            else break;
+            // ---- evaluate the first k candidates ----
+            uint32_t set = 0;
+            for (int r = 0; r < k; ++r) set |= 1u << ((ordl >> (4 * r)) & 15u);
+            long long pdbp = 0, psum = 0;
+            bool all_spot = true;
+            int tpods[MAXN][DMAX];
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) tpods[n][d] = npods[n][d];
+              if (set >> n & 1u) {
+                psum += nprice[n];
+                all_spot = all_spot && ni_cap(ninfo[n]) == 0;
+#pragma unroll
+                for (int d = 0; d < DMAX; ++d) if (d < D && dep[d].pdb) pdbp += npods[n][d];
+              }
+            }
+            bool ok = pdbp <= allowed;
+            uint32_t touched = 0;
+            const uint32_t recv = rdy & ~tn & ~set;
+            for (int r = 0; r < k && ok; ++r) {
+              const int c = (int)((ordl >> (4 * r)) & 15u);
+              int cp[DMAX];
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                cp[d] = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) if (n == c) cp[d] = tpods[n][d];
+              }
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                if (d >= D) break;
+                int need_d = cp[d];
+#pragma unroll
+                for (int m = 0; m < MAXN; ++m) {
+                  const uint32_t x = ninfo[m];
+                  if (need_d > 0 && (recv >> m & 1u) && (capbit(ni_cap(x)) & capsel[d])) {
+                    int f;
+                    if (DMAX == 1) {
+                      f = ncap[m] - tpods[m][0];
+                    } else {
+                      int sc = 0, sm = 0, sp = 0;
+#pragma unroll
+                      for (int e = 0; e < DMAX; ++e) {
+                        if (e >= D) break;
+                        sc += tpods[m][e] * dep[e].req_cpu;
+                        sm += tpods[m][e] * dep[e].req_mem;
+                        sp += tpods[m][e];
+                      }
+                      f = max(type_fit<DMAX>(L, ni_type(x), sc, sm, sp, dep[d].req_cpu, dep[d].req_mem), 0);
+                    }
+                    const int kk = min(f, need_d);
+                    if (kk > 0) { tpods[m][d] += kk; need_d -= kk; touched |= 1u << m; }
+                  }
+                }
+                cp[d] = need_d;
+              }
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n)
+                if (n == c) {
+#pragma unroll
+                  for (int d = 0; d < DMAX; ++d) tpods[n][d] = cp[d];
+                }
+            }
+            // leftover pods need one new node, strictly cheaper than the set
+            int s_cpu = 0, s_mem = 0, s_pods = 0;
+            uint32_t cm = 0, zm = 0;
+            int use = 0, limit = 0, usem = 0;
+            const int limitm = w->pools[q].limit_mem_mi;
+#pragma unroll
+            for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+              if (qq == q) { cm = pcm[qq]; zm = pzm[qq]; use = puse[qq]; limit = plimit[qq]; }
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (!(set >> n & 1u)) continue;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) {
+                if (d >= D || tpods[n][d] <= 0) continue;
+                cm &= capsel[d];
+                s_cpu += tpods[n][d] * dep[d].req_cpu;
+                s_mem += tpods[n][d] * dep[d].req_mem;
+                s_pods += tpods[n][d];
+              }
+            }
+            int bk = -1, bz = 0, bc = 0, bpr = 0;
+            const uint32_t fr = ~used & slot_mask;
+            if (ok && s_pods > 0) {
+              if (all_spot) cm &= ~(uint32_t)CCKA_CAP_SPOT;
+              ok = cm != 0 && fr != 0;
+              if (ok) {
+                if (limitm >= 0) usem = pool_mem(q);
+                find_offer(zm, cm, use, limit, usem, limitm, s_cpu, s_mem, s_pods, bk, bz, bc, bpr);
+                ok = bk >= 0 && (long long)bpr < psum;
+              }
+            }
+            if (!commit) {
+              if (ok) { bestk = k; lo = mid + 1; }
+              else hi = mid - 1;
+              continue;
+            }
+            // ---- commit: moves, emptied candidates leave now, the rest await the replacement ----
+            uint32_t srcm = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) npods[n][d] = tpods[n][d];
+              if (touched >> n & 1u) nlast[n] = t;
+            }
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (!(set >> n & 1u)) continue;
+              int left = 0;
+#pragma unroll
+              for (int d = 0; d < DMAX; ++d) left += d < D ? npods[n][d] : 0;
+              if (left > 0) srcm |= 1u << n;
+            }
+            uint32_t gone = set & ~srcm;
+            while (gone) {
+              const int n = __builtin_ctz(gone);
+              gone &= gone - 1u;
+              free_slot(n);
+              deletions++;
+              flags |= 4u;
+            }
+            if (s_pods > 0) launch_replacement(q, __builtin_ctz(fr), srcm, bk, bz, bc, bpr);
+            flags |= 64u;
+            allowed -= pdbp;
+            deleted += k;
+            any_deleted = true;
+            acted = true;
+            break;
+          }
+          return acted;
+        };
+        // ---- G1. ready replacements take over their sources' pods (SEMANTICS 3.G0, 3.G2, 3.G3):
+        // replacements in slot order, each one's sources in slot order ----
+        if (greplace || gdrift || gmulti) {
           uint32_t rm = 0;
 #pragma unroll
           for (int m = 0; m < MAXN; ++m) rm |= ((nsrc[m] != 0) && (rdy >> m & 1u) ? 1u : 0u) << m;
           while (rm) {
             const int m = __builtin_ctz(rm);
             rm &= rm - 1u;
-            int src = 0;
-            uint32_t xm = 0;
+            uint32_t sm = 0, xm = 0;
 #pragma unroll
-            for (int n = 0; n < MAXN; ++n) if (n == m) { src = nsrc[n] - 1; nsrc[n] = 0; xm = ninfo[n]; }
-            int sp[DMAX];
+            for (int n = 0; n < MAXN; ++n) if (n == m) { sm = nsrc[n]; nsrc[n] = 0; xm = ninfo[n]; }
+            rm &= ~sm;
+            while (sm) {
+              const int src = __builtin_ctz(sm);
+              sm &= sm - 1u;
+              int sp[DMAX];
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) {
-              sp[d] = 0;
+              for (int d = 0; d < DMAX; ++d) {
+                sp[d] = 0;
 #pragma unroll
-              for (int n = 0; n < MAXN; ++n) if (n == src) sp[d] = npods[n][d];
-            }
+                for (int n = 0; n < MAXN; ++n) if (n == src) sp[d] = npods[n][d];
+              }
 #pragma unroll
-            for (int d = 0; d < DMAX; ++d) {
-              if (d >= D) break;
-              int k = 0;
-              if (capbit(ni_cap(xm)) & capsel[d]) {
+              for (int d = 0; d < DMAX; ++d) {
+                if (d >= D) break;
+                int k = 0;
+                if (capbit(ni_cap(xm)) & capsel[d]) {
 #pragma unroll
-                for (int n = 0; n < MAXN; ++n) {
-                  if (n == m) {
-                    int f;
-                    if (DMAX == 1) {
-                      f = ncap[n] - npods[n][0];
-                    } else {
-                      int sc = 0, sm = 0, spp = 0;
+                  for (int n = 0; n < MAXN; ++n) {
+                    if (n == m) {
+                      int f;
+                      if (DMAX == 1) {
+                        f = ncap[n] - npods[n][0];
+                      } else {
+                        int sc = 0, smm = 0, spp = 0;
 #pragma unroll
-                      for (int e = 0; e < DMAX; ++e) {
-                        if (e >= D) break;
-                        sc += npods[n][e] * dep[e].req_cpu;
-                        sm += npods[n][e] * dep[e].req_mem;
-                        spp += npods[n][e];
+                        for (int e = 0; e < DMAX; ++e) {
+                          if (e >= D) break;
+                          sc += npods[n][e] * dep[e].req_cpu;
+                          smm += npods[n][e] * dep[e].req_mem;
+                          spp += npods[n][e];
+                        }
+                        f = max(type_fit<DMAX>(L, ni_type(xm), sc, smm, spp, dep[d].req_cpu, dep[d].req_mem), 0);
                       }
-                      f = max(type_fit<DMAX>(L, ni_type(xm), sc, sm, spp, dep[d].req_cpu, dep[d].req_mem), 0);
+                      k = min(f, sp[d]);
+                      npods[n][d] += k;
                     }
-                    k = min(f, sp[d]);
-                    npods[n][d] += k;
                   }
                 }
+                rpods[d] -= sp[d] - k;
+                placed[d] -= sp[d] - k;
               }
-              rpods[d] -= sp[d] - k;
-              placed[d] -= sp[d] - k;
+              free_slot(src);
+              deletions++;
             }
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) if (n == m) nlast[n] = t;
-            free_slot(src);
-            rm &= ~(1u << src);
-            deletions++;
             any_deleted = true;
             flags |= 4u;
           }
@@ -1299,7 +1480,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             for (int n = 0; n < MAXN; ++n) pq |= (ni_pool(ninfo[n]) == q ? 1u : 0u) << n;
             uint32_t srcm = 0;  // nodes whose pre-spun replacement is in flight wait for it
 #pragma unroll
-            for (int n = 0; n < MAXN; ++n) if (nsrc[n]) srcm |= 1u << (nsrc[n] - 1);
+            for (int n = 0; n < MAXN; ++n) srcm |= nsrc[n];
             uint32_t cand = dmask & rdy & pq & ~srcm;
             while (cand && deleted < budget) {
               const int best = __builtin_ctz(cand);
@@ -1378,7 +1559,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
 #pragma unroll
                     for (int d = 0; d < DMAX; ++d) npods[n][d] = d < D ? left[d] : 0;
                   }
-                launch_replacement(q, __builtin_ctz(fr), best, bk, bz, bc, bpr);
+                launch_replacement(q, __builtin_ctz(fr), 1u << best, bk, bz, bc, bpr);
                 allowed -= pdb_pods;
                 deleted++;
                 flags |= 16u;
@@ -1470,7 +1651,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               any_deleted = true;
               flags |= 4u;
             }
-            if (greplace && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
+            {
+              const bool g3 = gmulti && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED && try_multi(q, qca, budget, deleted);
+              if (greplace && !g3 && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
+            }
             continue;
           }
           uint32_t rejected = taint_mask();  // tainted nodes: neither candidates nor receivers
@@ -1589,7 +1773,10 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
             any_deleted = true;
             flags |= 4u;
           }
-          if (greplace && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
+          {
+            const bool g3 = gmulti && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED && try_multi(q, qca, budget, deleted);
+            if (greplace && !g3 && qpol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) try_replace(q, qca, budget, deleted);
+          }
         }
         bool pending_repl = false;
 #pragma unroll

@@ -44,7 +44,7 @@ static int usage() {
                "                   [--label KIND NAME 'k=v ...']...\n"
                "                   [--catalog tiny|small] [--steps T] [--max-nodes N] [--load-m M]\n"
                "                   [--device D] [--json OUT] [--prom OUT] [--csv OUT] [--start-unix-ms MS]\n"
-               "                   [--drift] [--replace] [--kyverno] [--hpa-sync S]\n");
+               "                   [--drift] [--replace] [--multi] [--kyverno] [--hpa-sync S]\n");
   return 2;
 }
 
@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
   long long start_ms = 0;
   std::vector<std::string> applies;
   std::vector<std::vector<std::string>> patches, labels;
-  int steps = 1440, max_nodes = 16, device = 0, drift = 0, replace = 0, kyverno = 0, hpa_sync = 0;
+  int steps = 1440, max_nodes = 16, device = 0, drift = 0, replace = 0, multi = 0, kyverno = 0, hpa_sync = 0;
   long load_m = 100;
   for (int a = 2; a < argc; ++a) {
     auto next = [&]() -> std::string {
@@ -143,6 +143,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[a], "--start-unix-ms")) start_ms = std::atoll(next().c_str());
     else if (!std::strcmp(argv[a], "--drift")) drift = 1;
     else if (!std::strcmp(argv[a], "--replace")) replace = 1;
+    else if (!std::strcmp(argv[a], "--multi")) multi = 1;
     else if (!std::strcmp(argv[a], "--kyverno")) kyverno = 1;
     else if (!std::strcmp(argv[a], "--hpa-sync")) hpa_sync = std::atoi(next().c_str());
     else return usage();
@@ -183,7 +184,8 @@ int main(int argc, char** argv) {
   ccka_world w;
   if (ccka_host_build_world(h, catalog.c_str(), steps, max_nodes, &w) != CCKA_OK) die_host(h, "build world");
   // Karpenter drift on the zone switch / replacement consolidation (SEMANTICS 3.G0, 3.G2)
-  w.disrupt_ext = (drift ? CCKA_DISRUPT_DRIFT : 0) | (replace ? CCKA_DISRUPT_REPLACE : 0);
+  w.disrupt_ext = (drift ? CCKA_DISRUPT_DRIFT : 0) | (replace ? CCKA_DISRUPT_REPLACE : 0) |
+                  (multi ? CCKA_DISRUPT_MULTI : 0);
   // kube-controller-manager --horizontal-pod-autoscaler-sync-period (upstream default 15 s;
   // 0 = one decision per 60-s step, SEMANTICS 3.C)
   w.hpa_sync_s = hpa_sync;

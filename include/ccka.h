@@ -69,6 +69,9 @@ enum { CCKA_POLICY_KEEP = 0, CCKA_WHEN_EMPTY = 1, CCKA_WHEN_EMPTY_OR_UNDERUTILIZ
 #define CCKA_DISRUPT_DRIFT 1    /* drift on a zone / capacity-type requirement change */
 #define CCKA_DISRUPT_REPLACE 2  /* single-node replacement consolidation (on-demand ->
                                    strictly cheaper offering, pre-spun replacement) */
+#define CCKA_DISRUPT_MULTI 4    /* multi-node consolidation: >= 2 nodes of a
+                                   WhenEmptyOrUnderutilized pool leave together, with at
+                                   most one cheaper replacement (SEMANTICS 3.G3) */
 enum { CCKA_SCALER_STATIC = 0, CCKA_SCALER_HPA = 1, CCKA_SCALER_KEDA = 2, CCKA_SCALER_KEDA_TRIGGER = 3 };
 enum { CCKA_PROFILE_RESET = 0, CCKA_PROFILE_OFFPEAK = 1, CCKA_PROFILE_PEAK = 2 };
 /* HPA behavior */

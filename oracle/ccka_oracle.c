@@ -222,7 +222,7 @@ int32_t ccka_oracle_hpa_behavior(int32_t cur, int32_t proposal, int32_t min_r, i
 /* ------------------------------------------------------------------------ */
 typedef struct {
   int used, pool, type, zone, cap, ready_step, last_event;
-  int src1;  /* replacement node: 1 + the slot it replaces (0: none) */
+  uint32_t srcm; /* replacement node: bit n = it replaces slot n (0: none) */
   int pods[CCKA_MAX_DEPLOY];
 } o_node;
 
@@ -361,7 +361,7 @@ typedef struct {
 static void o_free(o_node* nodes, int NN, int n) {
   memset(&nodes[n], 0, sizeof(o_node));
   for (int m = 0; m < NN; ++m)
-    if (nodes[m].src1 == n + 1) nodes[m].src1 = 0;
+    nodes[m].srcm &= ~(1u << n);
 }
 
 /* cheapest single offering (price, k, z, c) holding the sums under zone mask
@@ -424,8 +424,8 @@ static int o_launch_choice(const o_env* e, int r, int h, uint32_t zm, uint32_t c
   return bk;
 }
 
-/* a pre-spun replacement for slot src, no pods until it takes over */
-static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, int ready, int t, int src) {
+/* a pre-spun replacement for the slots in srcm, no pods until it takes over */
+static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, int ready, int t, uint32_t srcm) {
   o_node* nd = &st->nodes[slot];
   memset(nd, 0, sizeof *nd);
   nd->used = 1;
@@ -435,7 +435,7 @@ static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, 
   nd->cap = bc;
   nd->ready_step = ready;
   nd->last_event = t;
-  nd->src1 = src + 1;
+  nd->srcm = srcm;
   st->launches++;
   st->pool_launches[p]++;
   st->last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)p << 16;
@@ -447,9 +447,9 @@ static void o_launch_repl(o_state* st, int slot, int p, int bk, int bz, int bc, 
  * replacement (sized for the source's pods, SEMANTICS 3.G0/G2) receives other
  * pods until the takeover, and the source is no consolidation candidate. */
 static int o_tainted(const o_node* nodes, int NN, int n) {
-  if (nodes[n].src1) return 1;
+  if (nodes[n].srcm) return 1;
   for (int m = 0; m < NN; ++m)
-    if (nodes[m].used && nodes[m].src1 == n + 1) return 1;
+    if (nodes[m].used && (nodes[m].srcm >> n & 1u)) return 1;
   return 0;
 }
 
@@ -466,6 +466,72 @@ static o_use o_pool_use(const o_state* st, const ccka_world* w, int NN, int p) {
 static int o_drifted(const o_state* st, const o_node* nd) {
   const o_pool* pl = &st->pools[nd->pool];
   return !(pl->zone_mask >> nd->zone & 1u) || !(pl->cap_mask & (uint32_t)o_capidx_bit(nd->cap));
+}
+
+/* G3 trial (docs/SEMANTICS.md 3.G3): the first k candidates of `order` leave
+ * the cluster together. Their pods move first-fit (candidates in order,
+ * deployments in index order, receivers in slot order: ready, untainted,
+ * outside the set, capacity-type compatible) on a copy of the slots; what does
+ * not fit needs one new node: the cheapest offering (price, k, z, c) holding
+ * the leftover sums under the pool's zone mask, capacity types
+ * pool.cap_mask & the leftovers' nodeSelectors (no spot when every candidate is
+ * spot) and limits, strictly cheaper than the candidates together, in a free
+ * slot. Returns 1 when the set consolidates; *bk < 0: no new node needed. */
+static int o_g3_try(const o_env* e, const o_state* st, int r, int h, int p, const int* order, int k,
+                    const uint32_t* capsel, int64_t allowed, int t, o_node* trial, int* bk, int* bz, int* bc,
+                    int32_t* bp, int* slot, int64_t* pdb_out) {
+  const ccka_world* w = e->w;
+  const int D = e->D, NN = e->N;
+  uint32_t set = 0;
+  int all_spot = 1;
+  int64_t pdb_pods = 0, price_sum = 0;
+  for (int i = 0; i < k; ++i) {
+    const o_node* nd = &st->nodes[order[i]];
+    set |= 1u << order[i];
+    all_spot &= nd->cap == 0;
+    price_sum += o_price(e, r, h, nd->type, nd->zone, nd->cap);
+    for (int d = 0; d < D; ++d) if (w->deploy[d].pdb_member) pdb_pods += nd->pods[d];
+  }
+  *pdb_out = pdb_pods;
+  if (pdb_pods > allowed) return 0;
+  memcpy(trial, st->nodes, sizeof(o_node) * (size_t)NN);
+  for (int i = 0; i < k; ++i) {
+    o_node* cn = &trial[order[i]];
+    for (int d = 0; d < D; ++d) {
+      int need = cn->pods[d];
+      for (int m = 0; m < NN && need > 0; ++m) {
+        o_node* nd = &trial[m];
+        if ((set >> m & 1u) || !nd->used || nd->ready_step > t) continue;
+        if (o_tainted(st->nodes, NN, m)) continue;
+        if (!((uint32_t)o_capidx_bit(nd->cap) & capsel[d])) continue;
+        const int64_t f = o_node_fit(e, nd, d);
+        const int kk = (int)(f < need ? f : need);
+        if (kk > 0) { nd->pods[d] += kk; need -= kk; nd->last_event = t; }
+      }
+      cn->pods[d] = need;
+    }
+  }
+  int64_t sc = 0, sm = 0, sp = 0;
+  uint32_t cm = st->pools[p].cap_mask;
+  for (int i = 0; i < k; ++i)
+    for (int d = 0; d < D; ++d) {
+      const int left = trial[order[i]].pods[d];
+      if (left <= 0) continue;
+      cm &= capsel[d];
+      sc += (int64_t)left * w->deploy[d].req_cpu_m;
+      sm += (int64_t)left * w->deploy[d].req_mem_mi;
+      sp += left;
+    }
+  *bk = -1;
+  *slot = -1;
+  if (sp == 0) return 1;  /* delete only */
+  if (all_spot) cm &= ~(uint32_t)CCKA_CAP_SPOT;
+  if (!cm) return 0;
+  for (int m = 0; m < NN; ++m) if (!st->nodes[m].used) { *slot = m; break; }
+  if (*slot < 0) return 0;
+  const o_use use = o_pool_use(st, w, NN, p);
+  *bk = o_offer(e, r, h, st->pools[p].zone_mask, cm, use, &w->pools[p], sc, sm, sp, bz, bc, bp);
+  return *bk >= 0 && (int64_t)*bp < price_sum;
 }
 
 /* det (optional): the per-pool / base-group / per-deployment breakdown of
@@ -780,23 +846,28 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
     }
     /* ---- G. disruption ---- */
     {
-      /* G1. replacements that are ready take over their source node's pods
-       * (docs/SEMANTICS.md 3.G2), slot order; pods that no longer fit are
-       * evicted; the source is deleted */
-      for (int m = 0; (w->disrupt_ext & (CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE)) && m < NN; ++m) {
+      /* G1. replacements that are ready take over their sources' pods
+       * (docs/SEMANTICS.md 3.G2, 3.G3): replacements in slot order, each one's
+       * sources in slot order; pods that no longer fit are evicted; the
+       * sources are deleted */
+      for (int m = 0; (w->disrupt_ext & (CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE | CCKA_DISRUPT_MULTI)) && m < NN;
+           ++m) {
         o_node* rn = &st.nodes[m];
-        if (!rn->used || !rn->src1 || rn->ready_step > t) continue;
-        const int n = rn->src1 - 1;
-        rn->src1 = 0;
-        for (int d = 0; d < D; ++d) {
-          if (!((uint32_t)o_capidx_bit(rn->cap) & capsel[d])) continue;
-          const int64_t f = o_node_fit(e, rn, d);
-          const int k = (int)(f < st.nodes[n].pods[d] ? f : st.nodes[n].pods[d]);
-          if (k > 0) rn->pods[d] += k;
+        if (!rn->used || !rn->srcm || rn->ready_step > t) continue;
+        const uint32_t sm = rn->srcm;
+        rn->srcm = 0;
+        for (int n = 0; n < NN; ++n) {
+          if (!(sm >> n & 1u)) continue;
+          for (int d = 0; d < D; ++d) {
+            if (!((uint32_t)o_capidx_bit(rn->cap) & capsel[d])) continue;
+            const int64_t f = o_node_fit(e, rn, d);
+            const int k = (int)(f < st.nodes[n].pods[d] ? f : st.nodes[n].pods[d]);
+            if (k > 0) rn->pods[d] += k;
+          }
+          o_free(st.nodes, NN, n);
+          st.deletions++;
         }
         rn->last_event = t;
-        o_free(st.nodes, NN, n);
-        st.deletions++;
         flags |= 4;
       }
       int64_t allowed = O_BIG;
@@ -826,7 +897,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           o_node* dn = &st.nodes[n];
           if (!dn->used || dn->pool != p || dn->ready_step > t || !o_drifted(&st, dn)) continue;
           int src = 0;  /* its pre-spun replacement is in flight: wait for it */
-          for (int m = 0; m < NN; ++m) src |= st.nodes[m].src1 == n + 1;
+          for (int m = 0; m < NN; ++m) src |= (st.nodes[m].srcm >> n) & 1u;
           if (src) continue;
           int64_t pdb_pods = 0;
           for (int d = 0; d < D; ++d) if (w->deploy[d].pdb_member) pdb_pods += dn->pods[d];
@@ -870,7 +941,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
                                    wc1000, &bz, &bc, &bp);
             if (bk >= 0) {
               for (int d = 0; d < D; ++d) dn->pods[d] = left[d];
-              o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, n);
+              o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, 1u << n);
               step_last_type = (uint16_t)bk;
               allowed -= pdb_pods;
               deleted++;
@@ -931,12 +1002,82 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           st.deletions++;
           flags |= 4;
         }
+        /* G3. multi-node consolidation (docs/SEMANTICS.md 3.G3): Karpenter's
+         * firstN binary search over the candidate prefix (>= 2 nodes) that can
+         * leave together, with at most one cheaper replacement */
+        int g3_acted = 0;
+        if ((w->disrupt_ext & CCKA_DISRUPT_MULTI) && st.pools[p].policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED &&
+            deleted < budget) {
+          int order[CCKA_MAX_NODES], nc = 0;
+          uint32_t taken = 0;
+          for (;;) {
+            int best = -1, bpods = 0;
+            int32_t bprice = 0;
+            for (int n = 0; n < NN; ++n) {
+              const o_node* nd = &st.nodes[n];
+              if ((taken >> n & 1u) || !nd->used || nd->pool != p || nd->ready_step > t) continue;
+              if ((int64_t)(t - nd->last_event) * CCKA_STEP_SECONDS < st.pools[p].ca_s) continue;
+              if (o_tainted(st.nodes, NN, n)) continue;
+              int pods = 0;
+              for (int d = 0; d < D; ++d) pods += nd->pods[d];
+              if (pods == 0) continue;
+              const int32_t pr = o_price(e, r, h, nd->type, nd->zone, nd->cap);
+              if (best < 0 || pods < bpods || (pods == bpods && pr > bprice)) { best = n; bpods = pods; bprice = pr; }
+            }
+            if (best < 0) break;
+            taken |= 1u << best;
+            order[nc++] = best;
+          }
+          if (nc > budget - deleted) nc = budget - deleted;
+          int lo = 1, hi = nc - 1, bestk = 0;
+          o_node trial[CCKA_MAX_NODES];
+          int bk = -1, bz = 0, bc = 0, slot = -1;
+          int32_t bp = 0;
+          int64_t pdb_pods = 0;
+          while (lo <= hi) {
+            const int mid = (lo + hi) / 2;
+            if (o_g3_try(e, &st, r, h, p, order, mid + 1, capsel, allowed, t, trial, &bk, &bz, &bc, &bp, &slot,
+                         &pdb_pods)) {
+              bestk = mid + 1;
+              lo = mid + 1;
+            } else {
+              hi = mid - 1;
+            }
+          }
+          if (bestk) {
+            (void)o_g3_try(e, &st, r, h, p, order, bestk, capsel, allowed, t, trial, &bk, &bz, &bc, &bp, &slot,
+                           &pdb_pods);
+            memcpy(st.nodes, trial, sizeof(o_node) * (size_t)NN);
+            uint32_t srcm = 0;
+            for (int i = 0; i < bestk; ++i) {
+              const int n = order[i];
+              int pods = 0;
+              for (int d = 0; d < D; ++d) pods += st.nodes[n].pods[d];
+              if (pods > 0) {
+                srcm |= 1u << n;  /* leaves when the replacement is ready */
+              } else {
+                o_free(st.nodes, NN, n);
+                st.deletions++;
+                flags |= 4;
+              }
+            }
+            if (bk >= 0) {
+              o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, srcm);
+              step_last_type = (uint16_t)bk;
+              flags |= 2 | 32;
+            }
+            flags |= 64;
+            allowed -= pdb_pods;
+            deleted += bestk;
+            g3_acted = 1;
+          }
+        }
         /* G2. single-node replacement consolidation (docs/SEMANTICS.md 3.G2):
          * the first candidate (same order, on-demand, with pods, not already
          * being replaced) that has a strictly cheaper single offering for its
          * pods gets a pre-spun replacement; one per pool per step */
         int rej2[CCKA_MAX_NODES] = {0};
-        while ((w->disrupt_ext & CCKA_DISRUPT_REPLACE) &&
+        while ((w->disrupt_ext & CCKA_DISRUPT_REPLACE) && !g3_acted &&
                st.pools[p].policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED && deleted < budget) {
           int best = -1, bpods = 0;
           int32_t bprice = 0;
@@ -945,7 +1086,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
             if (!nd->used || nd->pool != p || nd->ready_step > t || rej2[n] || nd->cap != 1) continue;
             if ((int64_t)(t - nd->last_event) * CCKA_STEP_SECONDS < st.pools[p].ca_s) continue;
             int src = 0;
-            for (int m = 0; m < NN; ++m) src |= st.nodes[m].src1 == n + 1;
+            for (int m = 0; m < NN; ++m) src |= (st.nodes[m].srcm >> n) & 1u;
             if (src) continue;
             int pods = 0;
             for (int d = 0; d < D; ++d) pods += nd->pods[d];
@@ -974,7 +1115,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
           int32_t bp = 0;
           const int bk = o_offer(e, r, h, st.pools[p].zone_mask, cm, use, &w->pools[p], s_cpu, s_mem, s_pods, &bz, &bc, &bp);
           if (bk < 0 || bp >= bprice) { rej2[best] = 1; continue; }
-          o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, best);
+          o_launch_repl(&st, slot, p, bk, bz, bc, t + w->provision_delay_steps, t, 1u << best);
           step_last_type = (uint16_t)bk;
           flags |= 2 | 32;
           deleted++;
