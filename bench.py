@@ -47,7 +47,8 @@ def main():
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2)
     ap.add_argument("--n", type=int, default=None, help="scenarios (states) per GPU, overrides the config")
     ap.add_argument("--T", type=int, default=1440)
-    ap.add_argument("--mode", choices=["trajectory", "summary"], default=None)
+    ap.add_argument("--mode", choices=["trajectory", "summary", "policy"], default=None,
+                    help="config 5: 'policy' = the closed-loop policy rollout (MLP in the loop every step)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--drift", action="store_true",
@@ -106,10 +107,26 @@ def main():
 
     cfg = args.config
     if args.warmup is None:
-        args.warmup = 50 if cfg == 5 else 2
+        args.warmup = 50 if cfg == 5 and args.mode != "policy" else (1 if cfg == 5 else 2)
     T = args.T
     spec = sc = None
-    if cfg == 5:
+    policy = cfg == 5 and args.mode == "policy"
+    if policy:
+        # closed loop: every step featurize -> MLP (bf16 MFMA) -> actions -> one rollout step
+        N = args.n or 1_000_000
+        T = args.T if args.T != 1440 else 60
+        spec = configs.config2_world(n_steps=T)
+        sc = configs.hpa_scenarios(N, first_id=rank * N)
+        ws, bs = configs.mlp_weights(11)
+        eng.mlp_set_weights([configs.to_bf16_bits(w) for w in ws], bs)
+        eng.set_world(spec)
+        eng.set_scenarios(sc)
+        eng.gen_load(configs.trace_gen())
+        traj = False
+
+        def step_fn():
+            eng.policy_rollout(trajectory=False)
+    elif cfg == 5:
         N = args.n or 10_000_000
         ws, bs = configs.mlp_weights(11)
         eng.mlp_set_weights([configs.to_bf16_bits(w) for w in ws], bs)
@@ -160,7 +177,11 @@ def main():
     barrier()
     t0 = time.perf_counter()
     kms = []
-    if cfg == 5:
+    if policy:
+        for _ in range(args.steps):
+            step_fn()
+            kms.append(eng.kernel_ms())
+    elif cfg == 5:
         # back-to-back launches, one sync: the policy kernel is ~1 ms, and a
         # host round trip per launch lets the shader clock sag between them
         for _ in range(args.steps):
@@ -173,7 +194,7 @@ def main():
             kms.append(eng.kernel_ms())
     barrier()
     elapsed = time.perf_counter() - t0
-    if cfg == 5:  # per-launch average over the stream (launch gaps included: conservative)
+    if cfg == 5 and not policy:  # per-launch average over the stream (launch gaps included: conservative)
         kms = [elapsed * 1e3 / args.steps]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -181,9 +202,28 @@ def main():
         elapsed = float(t.item())
     K = args.steps
     avg_ms = sum(kms) / len(kms)
-    engine_id, table_ms = eng.last_engine() if cfg != 5 else (0, 0.0)
+    engine_id, table_ms = eng.last_engine() if cfg != 5 or policy else (0, 0.0)
 
-    if cfg == 5:
+    if policy:
+        value = world * N * T * K / elapsed
+        # dominant MFMA work: one MLP batch over the N states per rollout step
+        flops = MLP_FLOPS_PER_STATE * N * T
+        achieved = flops / (avg_ms * 1e-3) / 1e12
+        out = {
+            "metric": "policy-evaluated cluster-steps/sec (closed-loop MLP control policy)",
+            "value": value, "unit": "cluster-steps/s", "n_gpus": world, "steps": K,
+            "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16 MLP (fp32 accumulate) + int64/f64 rollout",
+            "data": "synthetic (on-device Philox traces, Xavier-uniform weights seed 11)",
+            "config": {"workload": f"config5 closed loop: {N} clusters x {T} steps, every step featurize -> "
+                                   "MLP 64->256->256->8 -> HPA target + carbon weight -> rollout step",
+                       "clusters_per_gpu": N, "steps": T, "parallelism": f"data-parallel x{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
+                         "kernel": "whole loop (mlp_kernel + policy_act_kernel + rollout_kernel per step)",
+                         "loop_ms_avg": avg_ms, "flops_per_loop": flops},
+        }
+    elif cfg == 5:
         value = world * N * K / elapsed
         flops = MLP_FLOPS_PER_STATE * N
         achieved = flops / (avg_ms * 1e-3) / 1e12

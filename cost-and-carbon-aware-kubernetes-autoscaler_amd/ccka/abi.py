@@ -215,6 +215,8 @@ def load_engine(path: str | None = None):
         "ccka_get_trajectory": (C.c_int, [vp, C.POINTER(TrajRec), C.c_int64]),
         "ccka_get_totals": (C.c_int, [vp, C.POINTER(Totals)]),
         "ccka_set_detail": (C.c_int, [vp, C.c_int32]),
+        "ccka_policy_rollout": (C.c_int, [vp, C.c_int32, C.c_int32]),
+        "ccka_get_policy_actions": (C.c_int, [vp, C.c_void_p, C.c_void_p, C.c_int64]),
         "ccka_get_detail": (C.c_int, [vp, C.c_void_p, C.c_int64]),
         "ccka_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "ccka_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
@@ -239,6 +241,7 @@ EXPORTED = [
     "ccka_allreduce_totals", "ccka_comm_info", "ccka_device_info", "ccka_get_grid_stats", "ccka_pareto_frontier",
     "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
     "ccka_mlp_forward_async", "ccka_mlp_get_actions", "ccka_set_detail", "ccka_get_detail",
+    "ccka_policy_rollout", "ccka_get_policy_actions",
 ]
 
 

@@ -111,6 +111,33 @@ class Engine:
         self._chk(self.lib.ccka_get_detail(self.ctx, a.ctypes.data, a.size), "ccka_get_detail")
         return a
 
+    # ---- closed-loop learned policy (config 5) ----
+    def policy_rollout(self, trajectory: bool = False, record: bool = False):
+        """ccka_policy_rollout: the MLP policy (mlp_set_weights) decides every
+        step's HPA target and carbon weight from the scenario state."""
+        self._chk(self.lib.ccka_policy_rollout(self.ctx, int(trajectory), int(record)), "ccka_policy_rollout")
+
+    def policy_actions(self):
+        """The recorded actions: (target [T][N] int16, carbon weight [T][N] float64)."""
+        tg = np.zeros((self.T, self.n), np.int16)
+        cw = np.zeros((self.T, self.n), np.float64)
+        self._chk(self.lib.ccka_get_policy_actions(self.ctx, tg.ctypes.data, cw.ctypes.data, tg.size),
+                  "ccka_get_policy_actions")
+        return tg, cw
+
+    def debug_policy_features(self, enable: bool = True):
+        """Internal test hook: record the policy features of every step."""
+        fn = self.lib.ccka_debug_policy_features
+        fn.argtypes = [C.c_void_p, C.c_int32]
+        self._chk(fn(self.ctx, int(enable)), "ccka_debug_policy_features")
+
+    def debug_get_policy_features(self) -> np.ndarray:
+        fn = self.lib.ccka_debug_get_policy_features
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        a = np.zeros((self.T + 1, self.n, 64), np.uint16)
+        self._chk(fn(self.ctx, a.ctypes.data, a.size), "ccka_debug_get_policy_features")
+        return a
+
     # ---- policy sweep (config 4) ----
     def grid_stats(self, grid_size: int) -> np.ndarray:
         ng = self.n // grid_size

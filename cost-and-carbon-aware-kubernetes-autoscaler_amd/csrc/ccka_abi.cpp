@@ -117,6 +117,19 @@ struct ccka_ctx {
   float* d_my = nullptr;
   int64_t mlp_n = 0, mlp_cap = 0;
   int last_engine = 0;       // 1 general, 2 single-deployment
+  // closed-loop policy rollout (config 5)
+  int32_t* d_pol_state = nullptr;
+  int64_t pol_state_count = 0;
+  int16_t* d_pol_target = nullptr;
+  double* d_pol_cw = nullptr;
+  int64_t pol_n = 0;
+  int16_t* d_rec_target = nullptr;
+  double* d_rec_cw = nullptr;
+  int64_t pol_rec_count = 0;
+  bool pol_rec_valid = false;
+  bool pol_feat_on = false;
+  uint16_t* d_feat_rec = nullptr;
+  int64_t pol_feat_count = 0;
   // per-scenario summary breakdown (ccka_set_detail)
   bool detail_on = false;
   bool detail_valid = false;
@@ -483,6 +496,8 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
   dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_ggather); dfree(c->d_gcounts); dfree(c->d_gn);
   dfree(c->d_gflags); dfree(c->d_gfront); dfree(c->d_hist);
+  dfree(c->d_pol_state); dfree(c->d_pol_target); dfree(c->d_pol_cw); dfree(c->d_rec_target); dfree(c->d_rec_cw);
+  dfree(c->d_feat_rec);
   dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -772,16 +787,17 @@ static int plan_launch(ccka_ctx* c, int* block, size_t* lds) {
   return CCKA_OK;
 }
 
-int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
-  if (!c) return CCKA_EINVAL;
-  if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
-  if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
-  (void)hipSetDevice(c->device);
+// the general kernel's parameters for a whole-horizon rollout: buffers,
+// launch geometry, HPA history, detail (shared by ccka_rollout_async and
+// ccka_policy_rollout)
+static int setup_general(ccka_ctx* c, int32_t trajectory, int* block_out, size_t* lds_out) {
   const ccka_world& w = c->hw;
   int block = 256;
   size_t lds = 0;
   int rc;
   if ((rc = plan_launch(c, &block, &lds)) != CCKA_OK) return rc;
+  *block_out = block;
+  *lds_out = lds;
   KParams& k = c->kp;
   k.w = c->d_world;
   k.types = c->d_types;
@@ -850,6 +866,11 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
       k.hist = c->d_hist;
     }
   }
+  k.t0 = 0;
+  k.t1 = w.n_steps;
+  k.state = nullptr;
+  k.state_load = 0;
+  k.feat = nullptr;
   k.N = c->N;
   k.NL = load_cols(c);
   k.trace_mod = c->n_traces;
@@ -862,6 +883,20 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
   k.P = w.n_pools;
   k.maxn = w.max_nodes;
   for (int d = 0; d < CCKA_MAX_DEPLOY; ++d) k.prov[d] = c->prov[d];
+  return CCKA_OK;
+}
+
+int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
+  if (!c) return CCKA_EINVAL;
+  if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
+  if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
+  (void)hipSetDevice(c->device);
+  const ccka_world& w = c->hw;
+  int block = 256;
+  size_t lds = 0;
+  int rc;
+  if ((rc = setup_general(c, trajectory, &block, &lds)) != CCKA_OK) return rc;
+  KParams& k = c->kp;
   if (c->engine_mode == 0 && c->d1_world && !c->d1_ready && (rc = d1_prepare(c)) != CCKA_OK) return rc;
   if (c->engine_mode == 0 && c->d1_world && c->d1_ok && !c->detail_on) {
     // single-deployment engine: argmin tables for this rollout, then the rollout
@@ -961,6 +996,152 @@ int ccka_rollout(ccka_ctx* c, int32_t trajectory) {
   int rc = ccka_rollout_async(c, trajectory);
   if (rc != CCKA_OK) return rc;
   return ccka_sync(c);
+}
+
+static int mlp_alloc(ccka_ctx* c, int64_t n);
+
+// ---- closed-loop learned control policy (config 5) ----
+// state words per scenario of the general kernel's persistence block (the
+// order of state_io in rollout.hip)
+static int64_t state_words(int dmax, int nmax) {
+  return (int64_t)dmax * (5 + 2 * CCKA_HIST) + 5 * CCKA_MAX_POOLS + (int64_t)nmax * (6 + dmax) + 36;
+}
+
+int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
+  if (!c) return CCKA_EINVAL;
+  if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
+  if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
+  if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
+  (void)hipSetDevice(c->device);
+  const ccka_world& w = c->hw;
+  const int64_t N = c->N;
+  const int T = w.n_steps;
+  int block = 256;
+  size_t lds = 0;
+  int rc;
+  if ((rc = setup_general(c, trajectory, &block, &lds)) != CCKA_OK) return rc;
+  KParams& k = c->kp;
+  int dmax, nmax;
+  kernel_dims(w.n_deploy, w.max_nodes, &dmax, &nmax);
+  const int64_t words = state_words(dmax, nmax);
+  if (c->pol_state_count < words * N) {
+    dfree(c->d_pol_state);
+    if (hipMalloc((void**)&c->d_pol_state, (size_t)(words * N) * 4) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "policy state alloc (%lld words)", (long long)(words * N));
+    c->pol_state_count = words * N;
+  }
+  if (c->pol_n < N) {
+    dfree(c->d_pol_target);
+    dfree(c->d_pol_cw);
+    if (hipMalloc((void**)&c->d_pol_target, (size_t)N * 2) != hipSuccess ||
+        hipMalloc((void**)&c->d_pol_cw, (size_t)N * 8) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "policy action alloc");
+    c->pol_n = N;
+  }
+  c->pol_rec_valid = false;
+  if (record) {
+    if (c->pol_rec_count < (int64_t)T * N) {
+      dfree(c->d_rec_target);
+      dfree(c->d_rec_cw);
+      if (hipMalloc((void**)&c->d_rec_target, (size_t)T * N * 2) != hipSuccess ||
+          hipMalloc((void**)&c->d_rec_cw, (size_t)T * N * 8) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "policy action record alloc");
+      c->pol_rec_count = (int64_t)T * N;
+    }
+  }
+  if (c->pol_feat_on) {
+    if (c->pol_feat_count < (int64_t)(T + 1) * N * 64) {
+      dfree(c->d_feat_rec);
+      if (hipMalloc((void**)&c->d_feat_rec, (size_t)(T + 1) * N * 64 * 2) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "policy feature record alloc");
+      c->pol_feat_count = (int64_t)(T + 1) * N * 64;
+    }
+  }
+  if ((rc = mlp_alloc(c, N)) != CCKA_OK) return rc;
+  MlpParams mp{};
+  mp.x = c->d_mx;
+  mp.y = c->d_my;
+  mp.w1f = c->d_w1f;
+  mp.w2f = c->d_w2f;
+  mp.w3f = c->d_w3f;
+  mp.b1 = c->d_mb;
+  mp.b2 = c->d_mb + MLP_HID;
+  mp.b3 = c->d_mb + 2 * MLP_HID;
+  mp.N = N;
+  mp.stamps = nullptr;
+  // the policy's actions replace the scenarios' target / carbon-weight overrides
+  k.target = c->d_pol_target;
+  k.cw = c->d_pol_cw;
+  k.state = c->d_pol_state;
+  k.feat = c->d_mx;
+  auto keep_feat = [&](int t) -> int {
+    if (!c->pol_feat_on) return CCKA_OK;
+    HIPCHK(c, hipMemcpyAsync(c->d_feat_rec + (size_t)t * N * 64, c->d_mx, (size_t)N * 64 * 2, hipMemcpyDeviceToDevice,
+                             c->stream));
+    return CCKA_OK;
+  };
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
+  // t = 0: initialise the state, features of step 0 (no step runs)
+  k.t0 = 0;
+  k.t1 = 0;
+  k.state_load = 0;
+  HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+  if ((rc = keep_feat(0)) != CCKA_OK) return rc;
+  for (int t = 0; t < T; ++t) {
+    HIPCHK(c, launch_mlp(mp, c->cus, c->stream));
+    HIPCHK(c, launch_policy_act(c->d_my, c->d_pol_target, c->d_pol_cw, record ? c->d_rec_target + (size_t)t * N : nullptr,
+                                record ? c->d_rec_cw + (size_t)t * N : nullptr, N, c->stream));
+    k.t0 = t;
+    k.t1 = t + 1;
+    k.state_load = 1;
+    HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+    if ((rc = keep_feat(t + 1)) != CCKA_OK) return rc;
+  }
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  // back to whole-horizon rollouts with the scenarios' own overrides
+  k.target = c->d_target;
+  k.cw = c->d_cw;
+  k.state = nullptr;
+  k.feat = nullptr;
+  k.t0 = 0;
+  k.t1 = T;
+  k.state_load = 0;
+  c->last_engine = 3;
+  c->traj_valid = trajectory != 0;
+  c->detail_valid = c->detail_on;
+  c->pol_rec_valid = record != 0;
+  c->ran = true;
+  return ccka_sync(c);
+}
+
+int ccka_get_policy_actions(ccka_ctx* c, int16_t* target, double* cw, int64_t count) {
+  if (!c || !target || !cw) return CCKA_EINVAL;
+  if (!c->pol_rec_valid) return fail(c, CCKA_ESTATE, "last run recorded no policy actions");
+  if (count != (int64_t)c->hw.n_steps * c->N) return fail(c, CCKA_EINVAL, "action count != T x N");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(target, c->d_rec_target, (size_t)count * 2, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(cw, c->d_rec_cw, (size_t)count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+// Internal test hooks (not part of include/ccka.h): record the policy
+// features of every step ([T + 1][N][64] bf16) and read them back.
+int ccka_debug_policy_features(ccka_ctx* c, int32_t enable) {
+  if (!c) return CCKA_EINVAL;
+  c->pol_feat_on = enable != 0;
+  return CCKA_OK;
+}
+
+int ccka_debug_get_policy_features(ccka_ctx* c, uint16_t* out, int64_t count) {
+  if (!c || !out) return CCKA_EINVAL;
+  if (!c->pol_feat_on || !c->pol_rec_valid) return fail(c, CCKA_ESTATE, "no recorded features");
+  if (count != (int64_t)(c->hw.n_steps + 1) * c->N * 64) return fail(c, CCKA_EINVAL, "feature count mismatch");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(out, c->d_feat_rec, (size_t)count * 2, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
 }
 
 int ccka_last_kernel_ms(ccka_ctx* c, double* ms) {

@@ -50,6 +50,14 @@ struct KParams {
   DetailDev* detail;    // nullable: per-scenario summary breakdown (ccka_set_detail)
   int2* hist;           // HBM decision history [hlen][D][N] {rec + 1 (0: none), delta}; hlen 0: register rings
   int32_t hlen, nsub, sync_s, _hpad;
+  // closed-loop policy rollout (ccka_policy_rollout): steps [t0, t1) of the
+  // horizon per launch; the scenario state persists in HBM between launches
+  // ([word][N] int32, SoA: coalesced), and the launch leaves the policy
+  // features of step t1 ([N][64] bf16, SEMANTICS 5)
+  int32_t t0, t1;
+  int32_t* state;        // nullable: no persistence (whole horizon in one launch)
+  int32_t state_load;    // 1: resume from `state` (else initialise from the world)
+  uint16_t* feat;        // nullable
   int64_t N;
   int64_t NL;           // load columns: N, or the shared trace count
   int64_t trace_mod;    // 0: column = scenario; else column = (first_id + i) % trace_mod
@@ -247,6 +255,9 @@ struct MlpParams {
 };
 hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s);
 hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipStream_t s);
+// policy actions -> the step's scaler parameters (SEMANTICS 5); rec_* nullable
+hipError_t launch_policy_act(const float* y, int16_t* target, double* cw, int16_t* rec_target, double* rec_cw,
+                             int64_t n, hipStream_t s);
 hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s);
 
 }  // namespace ccka

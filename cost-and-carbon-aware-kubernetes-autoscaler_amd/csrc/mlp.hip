@@ -288,6 +288,33 @@ hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s) {
   return hipGetLastError();
 }
 
+// The policy's action -> this step's scaler parameters (SEMANTICS 5): the
+// HPA target utilisation 60 + rint(16 y0) clamped to [20, 95] %, and the
+// Karpenter carbon weight rint(16 y1) / 16 clamped to [0, 4] $/kgCO2. Scaling by
+// 16 is exact in fp32 and rint rounds half to even, so the mapping is
+// reproducible from y on any IEEE host.
+__global__ void __launch_bounds__(256) policy_act_kernel(const float* __restrict__ y, int16_t* target, double* cw,
+                                                        int16_t* rec_target, double* rec_cw, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float q0 = rintf(y[i * 8 + 0] * 16.0f), q1 = rintf(y[i * 8 + 1] * 16.0f);
+  const int16_t tg = (int16_t)(60 + (int)fminf(fmaxf(q0, -40.0f), 35.0f));
+  const double c = (double)(int)fminf(fmaxf(q1, 0.0f), 64.0f) / 16.0;
+  target[i] = tg;
+  cw[i] = c;
+  if (rec_target) {
+    rec_target[i] = tg;
+    rec_cw[i] = c;
+  }
+}
+
+hipError_t launch_policy_act(const float* y, int16_t* target, double* cw, int16_t* rec_target, double* rec_cw,
+                             int64_t n, hipStream_t s) {
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(policy_act_kernel, dim3((unsigned)blocks), dim3(256), 0, s, y, target, cw, rec_target, rec_cw, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipStream_t s) {
   hipLaunchKernelGGL(mlp_gen_states_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, x, count, seed);
   return hipGetLastError();

@@ -327,6 +327,41 @@ __device__ __forceinline__ int rate_limit(const Rule& R, bool up, int cur, const
   return (int)res;
 }
 
+// ---- closed-loop policy rollout: state persistence and features ----
+// one 32-bit word per SoA row of the state block (8-byte values take two rows)
+template <class T>
+__device__ __forceinline__ void st_xfer(T& v, int32_t* st, int& k, int64_t N, int64_t i, bool save) {
+  if constexpr (sizeof(T) == 8) {
+    int32_t w2[2];
+    if (save) {
+      __builtin_memcpy(w2, &v, 8);
+      st[(int64_t)k * N + i] = w2[0];
+      st[(int64_t)(k + 1) * N + i] = w2[1];
+    } else {
+      w2[0] = st[(int64_t)k * N + i];
+      w2[1] = st[(int64_t)(k + 1) * N + i];
+      __builtin_memcpy(&v, w2, 8);
+    }
+    k += 2;
+  } else if constexpr (sizeof(T) == 4) {
+    int32_t x;
+    if (save) { __builtin_memcpy(&x, &v, 4); st[(int64_t)k * N + i] = x; }
+    else { x = st[(int64_t)k * N + i]; __builtin_memcpy(&v, &x, 4); }
+    k += 1;
+  } else {
+    if (save) st[(int64_t)k * N + i] = v ? 1 : 0;
+    else v = st[(int64_t)k * N + i] != 0;
+    k += 1;
+  }
+}
+
+// float -> bf16 bits, round to nearest even (finite inputs)
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t b;
+  __builtin_memcpy(&b, &f, 4);
+  return (uint16_t)((b + 0x7FFFu + ((b >> 16) & 1u)) >> 16);
+}
+
 // decision-history entries inside a window / period: entry k is (k + 1) * sync_s old
 __device__ __forceinline__ int hist_n(int window_s, int sync_s) { return window_s > sync_s ? (window_s - 1) / sync_s : 0; }
 
@@ -577,12 +612,99 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   const int64_t lcol = !active ? 0 : (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
   const int32_t* lptr = p.load + lcol;
   const int64_t lstride = p.NL;
-#pragma unroll
-  for (int d = 0; d < DMAX; ++d) Lnext[d] = lptr[(d < D ? d : 0) * lstride];
-  int minute = gw->start_minute % 1440;
   int hour = -1;
 
-  for (int t = 0; t < p.T; ++t, minute = minute == 1439 ? 0 : minute + 1) {
+  // ---- persisted state (closed-loop policy rollout): the loop-carried
+  // variables in one fixed order, loaded before the first step of a resumed
+  // launch and saved after its last ----
+  auto state_io = [&](bool save) {
+    int32_t* st = p.state;
+    const int64_t sN = p.N;
+    int k = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      st_xfer(replicas[d], st, k, sN, i, save);
+      st_xfer(last_active[d], st, k, sN, i, save);
+      st_xfer(placed[d], st, k, sN, i, save);
+      st_xfer(rpods[d], st, k, sN, i, save);
+      st_xfer(recv[d], st, k, sN, i, save);
+#pragma unroll
+      for (int h = 0; h < CCKA_HIST; ++h) {
+        st_xfer(rec[d][h], st, k, sN, i, save);
+        st_xfer(delta[d][h], st, k, sN, i, save);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
+      st_xfer(ppol[q], st, k, sN, i, save);
+      st_xfer(pca[q], st, k, sN, i, save);
+      st_xfer(puse[q], st, k, sN, i, save);
+      st_xfer(pzm[q], st, k, sN, i, save);
+      st_xfer(pcm[q], st, k, sN, i, save);
+    }
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n) {
+      st_xfer(ninfo[n], st, k, sN, i, save);
+      st_xfer(nsrc[n], st, k, sN, i, save);
+      st_xfer(nready[n], st, k, sN, i, save);
+      st_xfer(nlast[n], st, k, sN, i, save);
+      st_xfer(nprice[n], st, k, sN, i, save);
+      st_xfer(ncap[n], st, k, sN, i, save);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) st_xfer(npods[n][d], st, k, sN, i, save);
+    }
+    st_xfer(used, st, k, sN, i, save);
+    st_xfer(rdy, st, k, sN, i, save);
+    st_xfer(next_ready, st, k, sN, i, save);
+    st_xfer(nsp, st, k, sN, i, save);
+    st_xfer(nod, st, k, sN, i, save);
+    st_xfer(g_dirty, st, k, sN, i, save);
+    st_xfer(g_wake, st, k, sN, i, save);
+    st_xfer(profile, st, k, sN, i, save);
+    st_xfer(cost, st, k, sN, i, save);
+    st_xfer(pend_min, st, k, sN, i, save);
+    st_xfer(burn, st, k, sN, i, save);
+    st_xfer(base_price, st, k, sN, i, save);
+    st_xfer(energy_nw, st, k, sN, i, save);
+    st_xfer(e_hour, st, k, sN, i, save);
+    st_xfer(gco2, st, k, sN, i, save);
+    st_xfer(ci_gpwmin, st, k, sN, i, save);
+    st_xfer(ci_gpwh, st, k, sN, i, save);
+    st_xfer(slo, st, k, sN, i, save);
+    st_xfer(nmin_spot, st, k, sN, i, save);
+    st_xfer(nmin_od, st, k, sN, i, save);
+    st_xfer(launches, st, k, sN, i, save);
+    st_xfer(deletions, st, k, sN, i, save);
+    st_xfer(peak_nodes, st, k, sN, i, save);
+    st_xfer(last_choice, st, k, sN, i, save);
+    st_xfer(hash, st, k, sN, i, save);
+    st_xfer(hpos, st, k, sN, i, save);
+    st_xfer(hour, st, k, sN, i, save);
+  };
+  const int t0 = p.t0, t1 = p.t1;
+  if (p.state && p.state_load) {
+    if (active) state_io(false);
+    // the hour's price tiles (block-uniform: every lane is at the same minute)
+    const int h0 = ((gw->start_minute + t0) % 1440) / 60;
+    if (p.all_hours) {
+      L.tile = tile_base + h0 * tile_ints;
+    } else {
+      for (int rr = 0; rr < p.span; ++rr) {
+        const int rg = L.rmin + rr;
+        if (rg >= p.R) break;
+        const int* src = p.price + ((int64_t)rg * 24 + h0) * tile_ints;
+        for (int x = tid; x < tile_ints; x += blockDim.x) tile_base[rr * tile_ints + x] = src[x];
+      }
+      __syncthreads();
+    }
+    // inactive lanes follow the block's hour sequence (the restage barrier is block-uniform)
+    if (!active) hour = t0 > 0 ? ((gw->start_minute + t0 - 1) % 1440) / 60 : -1;
+  }
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) Lnext[d] = lptr[((int64_t)min(t0, p.T - 1) * D + (d < D ? d : 0)) * lstride];
+  int minute = (gw->start_minute + t0) % 1440;
+
+  for (int t = t0; t < t1; ++t, minute = minute == 1439 ? 0 : minute + 1) {
     int Lcur[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
@@ -1874,8 +1996,47 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
     }
   }
   if (!active) return;
-  gco2 += (double)e_hour * (ci_gpwmin * 1e-9);
-  if (det) {
+  if (p.state) state_io(true);
+  if (p.feat) {
+    // policy features of step t1 (SEMANTICS 5): integers scaled by powers of
+    // two (exact in fp32), rounded to bf16 -- the oracle computes the same bits
+    uint16_t* f = p.feat + i * 64;
+    int reps = 0, rd = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      if (d < D) { reps += replicas[d]; rd += rpods[d]; }
+    const int tf = min(t1, p.T - 1);
+    const int mf = (gw->start_minute + t1) % 1440, hf = mf / 60;
+    const bool pk = pswitch && (ps <= pe ? (mf >= ps && mf < pe) : (mf >= ps || mf < pe));
+    float v[34];
+    v[0] = 1.0f;
+    v[1] = (float)reps * 0.0625f;
+    v[2] = (float)rd * 0.0625f;
+    v[3] = (float)(reps - rd) * 0.0625f;
+    v[4] = (float)lptr[((int64_t)tf * D) * lstride] * (1.0f / 1024.0f);
+    v[5] = (float)nsp;
+    v[6] = (float)nod;
+    v[7] = pk ? 1.0f : 0.0f;
+    v[8] = (float)s_ci[(rl * 24 + hf) * 2 + 1];
+    v[9] = (float)burn * (1.0f / 65536.0f);
+#pragma unroll
+    for (int h = 0; h < 24; ++h) v[10 + h] = h == hf ? 1.0f : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 34; ++j) f[j] = f2bf(v[j]);
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      int pods = 0, code = 0;
+      if (n < MAXN && (used >> n & 1u)) {
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n < MAXN ? n : 0][d] : 0;
+        code = 1 + ni_cap(ninfo[n < MAXN ? n : 0]) + ((rdy >> n & 1u) ? 0 : 2);
+      }
+      f[34 + n] = f2bf((float)pods * 0.0625f);
+      if (n < 14) f[50 + n] = f2bf((float)code);
+    }
+  }
+  if (t1 == p.T) gco2 += (double)e_hour * (ci_gpwmin * 1e-9);  // the last hour's carbon (run outputs only)
+  if (det && t1 == p.T) {
     for (int q = 0; q < NP; ++q) {
       det->d.pool_gco2[q] += (double)det->e_hour[q] * (ci_gpwmin * 1e-9);
       int cnt = 0;

@@ -370,6 +370,19 @@ int ccka_mlp_forward_async(ccka_ctx* ctx);
 /* Copy the actions [n][out_dim] fp32 back. */
 int ccka_mlp_get_actions(ccka_ctx* ctx, float* y, int64_t n);
 
+/* Closed-loop policy rollout (config 5): the learned policy in the loop.
+ * Before every step t the engine writes each scenario's 64 policy features
+ * (bf16, SEMANTICS 5), runs the MLP on all of them (bf16 MFMA, the weights of
+ * ccka_mlp_set_weights) and maps each scenario's actions to step t's scaler
+ * parameters: HPA target utilisation 60 + rint(16 y0) clamped to 20..95 % and
+ * Karpenter carbon weight rint(16 y1)/16 clamped to 0..4 $/kgCO2 (they replace
+ * the scenarios' target_util_pct / carbon_weight overrides). World, scenarios
+ * and load as ccka_rollout; results / trajectory / totals / detail read back
+ * the same way. record != 0 keeps the actions of every step. */
+int ccka_policy_rollout(ccka_ctx* ctx, int32_t trajectory, int32_t record);
+/* The recorded actions: target [T][N] int16 (%), cw [T][N] double ($/kg). */
+int ccka_get_policy_actions(ccka_ctx* ctx, int16_t* target, double* cw, int64_t count);
+
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------- */
 /* Fill a 128-byte RCCL unique id (rank 0 only; distribute it out of band). */
 int ccka_comm_unique_id(uint8_t* id128);

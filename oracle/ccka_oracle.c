@@ -534,10 +534,70 @@ static int o_g3_try(const o_env* e, const o_state* st, int r, int h, int p, cons
   return *bk >= 0 && (int64_t)*bp < price_sum;
 }
 
+static uint16_t o_bf16(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return (uint16_t)((b + 0x7FFFu + ((b >> 16) & 1u)) >> 16);
+}
+
+/* The 64 policy features of a scenario before step t1 (docs/SEMANTICS.md 5),
+ * bit-identical to the engine's (integers scaled by powers of two, fp32, bf16
+ * round-to-nearest-even). */
+static void o_features(const o_env* e, const o_state* st, const int32_t* load, int64_t nl, int64_t col, int r,
+                       int pswitch, int t1, uint16_t* f) {
+  const ccka_world* w = e->w;
+  const int D = e->D, NN = e->N, T = e->T;
+  int reps = 0, rd = 0;
+  for (int d = 0; d < D; ++d) {
+    reps += st->dep[d].replicas;
+    for (int n = 0; n < NN; ++n)
+      if (st->nodes[n].used && st->nodes[n].ready_step <= t1 - 1) rd += st->nodes[n].pods[d];
+  }
+  const int tf = t1 < T ? t1 : T - 1;
+  const int mf = (w->start_minute + t1) % 1440, hf = mf / 60;
+  const int ps = w->peak_start_min, pe = w->peak_end_min;
+  const int in_win = ps <= pe ? (mf >= ps && mf < pe) : (mf >= ps || mf < pe);
+  int64_t burn = 0;
+  int nsp = 0, nod = 0;
+  const int hp = t1 > 0 ? ((w->start_minute + t1 - 1) % 1440) / 60 : 0;
+  for (int n = 0; n < NN; ++n) {
+    const o_node* nd = &st->nodes[n];
+    if (!nd->used) continue;
+    burn += o_price(e, r, hp, nd->type, nd->zone, nd->cap);
+    if (nd->cap == 0) nsp++; else nod++;
+  }
+  float v[34];
+  v[0] = 1.0f;
+  v[1] = (float)reps * 0.0625f;
+  v[2] = (float)rd * 0.0625f;
+  v[3] = (float)(reps - rd) * 0.0625f;
+  v[4] = (float)load[((int64_t)tf * D) * nl + col] * (1.0f / 1024.0f);
+  v[5] = (float)nsp;
+  v[6] = (float)nod;
+  v[7] = (pswitch && in_win) ? 1.0f : 0.0f;
+  v[8] = (float)w->ci_gpwh[r * 24 + hf];
+  v[9] = (float)burn * (1.0f / 65536.0f);
+  for (int h = 0; h < 24; ++h) v[10 + h] = h == hf ? 1.0f : 0.0f;
+  for (int j = 0; j < 34; ++j) f[j] = o_bf16(v[j]);
+  for (int n = 0; n < 16; ++n) {
+    int pods = 0, code = 0;
+    if (n < NN && st->nodes[n].used) {
+      for (int d = 0; d < D; ++d) pods += st->nodes[n].pods[d];
+      code = 1 + st->nodes[n].cap + (st->nodes[n].ready_step <= t1 - 1 ? 0 : 2);
+    }
+    f[34 + n] = o_bf16((float)pods * 0.0625f);
+    if (n < 14) f[50 + n] = o_bf16((float)code);
+  }
+}
+
 /* det (optional): the per-pool / base-group / per-deployment breakdown of
  * ccka_detail, accounted exactly as the run totals (SEMANTICS 3.H) */
+/* act_t / act_cw (optional, [T][nsc]): the closed-loop policy's per-step HPA
+ * target utilisation and carbon weight (SEMANTICS 5); feat (optional,
+ * [T + 1][nsc][64]): the policy features before every step and after the last */
 static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* load, int64_t i,
-                      int64_t nsc, ccka_results* out, ccka_traj_rec* traj, ccka_detail* det) {
+                      int64_t nsc, ccka_results* out, ccka_traj_rec* traj, ccka_detail* det,
+                      const int16_t* act_t, const double* act_cw, uint16_t* feat) {
   const ccka_world* w = e->w;
   const int D = e->D, NN = e->N;
   o_state st;
@@ -553,7 +613,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
   const int reset_ca = sc->reset_ca_s ? sc->reset_ca_s[i] : w->reset_ca_s;
   const int pswitch = sc->peak_switch ? sc->peak_switch[i] : w->peak_switch;
   const double cw = sc->carbon_weight ? sc->carbon_weight[i] : w->carbon_weight;
-  const double wc1000 = cw * 1000.0;
+  double wc1000 = cw * 1000.0;
   int target[CCKA_MAX_DEPLOY], maxr[CCKA_MAX_DEPLOY];
   uint32_t capsel[CCKA_MAX_DEPLOY];
   ccka_hpa_rules downr[CCKA_MAX_DEPLOY];
@@ -598,6 +658,12 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
   if (det) memset(det, 0, sizeof *det);
 
   for (int t = 0; t < w->n_steps; ++t) {
+    if (feat) o_features(e, &st, load, nl, col, r, pswitch, t, feat + ((int64_t)t * nsc + i) * 64);
+    if (act_t) {  /* this step's policy action */
+      for (int d = 0; d < D; ++d)
+        if (w->deploy[d].scaler == CCKA_SCALER_HPA) target[d] = act_t[(int64_t)t * nsc + i];
+      wc1000 = act_cw[(int64_t)t * nsc + i] * 1000.0;
+    }
     const int minute = (w->start_minute + t) % 1440;
     const int h = minute / 60;
     /* carbon is charged per clock hour (SEMANTICS §3.H) */
@@ -1199,6 +1265,7 @@ static void o_run_one(const o_env* e, const ccka_scenarios* sc, const int32_t* l
       }
     }
   }
+  if (feat) o_features(e, &st, load, nl, col, r, pswitch, w->n_steps, feat + ((int64_t)w->n_steps * nsc + i) * 64);
   if (prev_h >= 0) st.gco2 += (double)st.e_hour * (w->ci_gpwmin[r * 24 + prev_h] * 1e-9);
   if (det && prev_h >= 0) {
     for (int p = 0; p < w->n_pools; ++p) {
@@ -1244,22 +1311,33 @@ typedef struct {
   ccka_results* out;
   ccka_traj_rec* traj;
   ccka_detail* detail;
+  const int16_t* act_t;
+  const double* act_cw;
+  uint16_t* feat;
   int64_t lo, hi;
 } o_job;
 
 static void* o_worker(void* arg) {
   o_job* j = (o_job*)arg;
-  for (int64_t i = j->lo; i < j->hi; ++i) o_run_one(j->e, j->sc, j->load, i, j->sc->n, j->out, j->traj, j->detail ? &j->detail[i] : NULL);
+  for (int64_t i = j->lo; i < j->hi; ++i) o_run_one(j->e, j->sc, j->load, i, j->sc->n, j->out, j->traj, j->detail ? &j->detail[i] : NULL, j->act_t,
+                                                 j->act_cw, j->feat);
   return NULL;
 }
 
 int ccka_oracle_rollout(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
                         ccka_results* out, ccka_traj_rec* traj, int32_t n_threads) {
-  return ccka_oracle_rollout_detail(w, sc, load, out, traj, NULL, n_threads);
+  return ccka_oracle_rollout_policy(w, sc, load, out, traj, NULL, NULL, NULL, NULL, n_threads);
 }
 
 int ccka_oracle_rollout_detail(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
                                ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, int32_t n_threads) {
+  return ccka_oracle_rollout_policy(w, sc, load, out, traj, detail, NULL, NULL, NULL, n_threads);
+}
+
+int ccka_oracle_rollout_policy(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
+                               ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, const int16_t* act_target,
+                               const double* act_cw, uint16_t* feat, int32_t n_threads) {
+  if ((act_target == NULL) != (act_cw == NULL)) return CCKA_EINVAL;
   if (!w || !sc || !load || !out || w->n_deploy < 1 || w->n_deploy > CCKA_MAX_DEPLOY ||
       w->max_nodes < 1 || w->max_nodes > CCKA_MAX_NODES || w->n_types < 1 || w->n_zones < 1 ||
       w->n_zones > CCKA_MAX_ZONES || w->n_pools < 1 || w->n_pools > CCKA_MAX_POOLS)
@@ -1299,6 +1377,9 @@ int ccka_oracle_rollout_detail(const ccka_world* w, const ccka_scenarios* sc, co
     jobs[k].out = out;
     jobs[k].traj = traj;
     jobs[k].detail = detail;
+    jobs[k].act_t = act_target;
+    jobs[k].act_cw = act_cw;
+    jobs[k].feat = feat;
     jobs[k].lo = sc->n * k / n_threads;
     jobs[k].hi = sc->n * (k + 1) / n_threads;
   }

@@ -29,6 +29,14 @@ int ccka_oracle_rollout(const ccka_world* w, const ccka_scenarios* sc, const int
 int ccka_oracle_rollout_detail(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
                                ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, int32_t n_threads);
 
+/* Closed-loop policy replay (SEMANTICS 5): act_target / act_cw ([T][sc->n])
+ * set every step's HPA target utilisation and carbon weight; feat (optional,
+ * [T + 1][sc->n][64] bf16) receives the policy features before every step and
+ * after the last. */
+int ccka_oracle_rollout_policy(const ccka_world* w, const ccka_scenarios* sc, const int32_t* load,
+                               ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, const int16_t* act_target,
+                               const double* act_cw, uint16_t* feat, int32_t n_threads);
+
 /* Serial totals over results (fixed scenario order). */
 void ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* out);
 

@@ -52,6 +52,11 @@ def lib():
         L.ccka_oracle_rollout_detail.argtypes = [C.POINTER(abi.World), C.POINTER(abi.Scenarios),
                                                  C.POINTER(C.c_int32), C.POINTER(abi.Results),
                                                  C.POINTER(abi.TrajRec), C.c_void_p, C.c_int32]
+        L.ccka_oracle_rollout_policy.restype = C.c_int
+        L.ccka_oracle_rollout_policy.argtypes = [C.POINTER(abi.World), C.POINTER(abi.Scenarios),
+                                                 C.POINTER(C.c_int32), C.POINTER(abi.Results),
+                                                 C.POINTER(abi.TrajRec), C.c_void_p, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p, C.c_int32]
         L.ccka_oracle_totals.argtypes = [C.POINTER(abi.Results), C.c_int64, C.POINTER(abi.Totals)]
         L.ccka_oracle_hpa_resource_proposal.restype = C.c_int32
         L.ccka_oracle_hpa_resource_proposal.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_int32,
@@ -110,6 +115,38 @@ def rollout_world(world, scen, load, traj=False, threads=1, detail=False, spec=N
     if rc != 0:
         raise abi.CckaError(f"oracle rollout failed: {rc}")
     return (arrays, tr, det) if detail else (arrays, tr)
+
+
+def rollout_policy(spec, scen, load, act_target, act_cw, traj=False, threads=1, features=False):
+    """Replay a closed-loop policy run (SEMANTICS 5): act_target / act_cw are the
+    per-step actions [T][N]. Returns (results, trajectory or None, features
+    [T + 1][N][64] uint16 bf16 bits or None)."""
+    w = spec.to_c()
+    s = scen.to_c()
+    load = np.ascontiguousarray(load, np.int32)
+    at = np.ascontiguousarray(act_target, np.int16)
+    ac = np.ascontiguousarray(act_cw, np.float64)
+    assert at.shape == (spec.n_steps, scen.n) and ac.shape == at.shape
+    arrays, r = alloc_results(scen.n)
+    tr = np.zeros((spec.n_steps, scen.n), TRAJ_DTYPE) if traj else None
+    ft = np.zeros((spec.n_steps + 1, scen.n, 64), np.uint16) if features else None
+    rc = lib().ccka_oracle_rollout_policy(C.byref(w), C.byref(s), load.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          C.byref(r), tr.ctypes.data_as(C.POINTER(abi.TrajRec)) if traj else None,
+                                          None, at.ctypes.data, ac.ctypes.data,
+                                          ft.ctypes.data if features else None, threads)
+    if rc != 0:
+        raise abi.CckaError(f"oracle policy rollout failed: {rc}")
+    return arrays, tr, ft
+
+
+def policy_act(y):
+    """The action mapping of SEMANTICS 5 in numpy (fp32, round half to even)."""
+    y = np.asarray(y, np.float32)
+    q0 = np.rint(y[..., 0] * np.float32(16.0))
+    q1 = np.rint(y[..., 1] * np.float32(16.0))
+    target = (60 + np.clip(q0, -40, 35)).astype(np.int16)
+    cw = np.clip(q1, 0, 64).astype(np.float64) / 16.0
+    return target, cw
 
 
 def totals(arrays, n):

@@ -1,0 +1,90 @@
+"""Closed-loop learned control policy (BASELINE config 5; SEMANTICS 5): the
+MLP decides every step's HPA target utilisation and Karpenter carbon weight
+from the scenario state. Parity is split where the arithmetic allows it:
+the features and the rollout under the recorded actions are bit-exact against
+the CPU oracle; the MLP itself is checked against a PyTorch fp32 reference
+(the actions derived from it agree except within rounding of an action
+boundary); the action mapping is reproduced in numpy."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+from ccka import abi, configs
+from parity import compare
+
+THREADS = 16
+
+
+def _case(n=512, T=180, drift=0):
+    spec = configs.config2_world(n_steps=T)
+    spec.drift = drift
+    sc = configs.hpa_scenarios(n, first_id=99)
+    load = po.gen_load(configs.trace_gen(5), T, 1, n, first_id=99)
+    return spec, sc, load
+
+
+def test_action_mapping_bounds():
+    y = np.array([[0.0, 0.0], [0.03125, 0.03125], [0.09375, -1.0], [10.0, 10.0], [-10.0, 0.2]], np.float32)
+    t, c = po.policy_act(np.pad(y, ((0, 0), (0, 6))))
+    assert t.tolist() == [60, 60, 62, 95, 20]  # rint(0.5) = 0, rint(1.5) = 2 (half to even)
+    assert c.tolist() == [0.0, 0.0, 0.0, 4.0, 0.1875]
+
+
+def test_oracle_replay_matches_fixed_overrides():
+    """Constant actions reproduce the ordinary rollout with the same per-scenario
+    overrides (the replay path is the rollout, not a second model)."""
+    spec, sc, load = _case(n=200, T=120)
+    tg = np.asarray(sc.target_util_pct, np.int16)
+    cw = np.full(sc.n, 0.5)
+    at = np.broadcast_to(tg, (spec.n_steps, sc.n)).copy()
+    ac = np.broadcast_to(cw, (spec.n_steps, sc.n)).copy()
+    r1, t1, f1 = po.rollout_policy(spec, sc, load, at, ac, traj=True, threads=8, features=True)
+    sc.carbon_weight = cw
+    r0, t0 = po.rollout(spec, sc, load, traj=True, threads=8)
+    compare(r1, r0, t1, t0)
+    # features: bias, hour one-hot, and the replica count match the trajectory
+    bf = configs.from_bf16_bits(f1)
+    assert (bf[:, :, 0] == 1.0).all() and (bf[:, :, 10:34].sum(-1) == 1.0).all()
+    assert np.array_equal(bf[1:, :, 1] * 16, t0["replicas"].astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("drift", [0, 1])
+def test_closed_loop_policy_parity(engine, drift):
+    import torch
+    from test_gpu_mlp import torch_ref
+    spec, sc, load = _case(drift=drift)
+    ws, bs = configs.mlp_weights(11)
+    wb = [configs.to_bf16_bits(w) for w in ws]
+    engine.set_world(spec)
+    engine.set_scenarios(sc)
+    engine.set_load(load)
+    engine.mlp_set_weights(wb, bs)
+    engine.debug_policy_features(True)
+    try:
+        engine.policy_rollout(trajectory=True, record=True)
+        rg = engine.results()
+        tg = engine.trajectory()
+        at, ac = engine.policy_actions()
+        fg = engine.debug_get_policy_features()
+    finally:
+        engine.debug_policy_features(False)
+    assert engine.last_engine()[0] == 3
+    assert at.std() > 0 and len(np.unique(at)) >= 3  # the policy really steers
+    # 1. the rollout under the recorded actions and every step's features: bit-exact
+    rc, tc, fc = po.rollout_policy(spec, sc, load, at, ac, traj=True, threads=THREADS, features=True)
+    compare(rg, rc, tg, tc)
+    bad = np.argwhere(fg != fc)
+    assert bad.size == 0, f"features differ at (t, i, f) {bad[:5].tolist()}"
+    # 2. the MLP on those features vs PyTorch fp32, through the action mapping
+    torch.manual_seed(0)
+    steps = [0, spec.n_steps // 2, spec.n_steps - 1]
+    for t in steps:
+        y = torch_ref(fg[t], wb, bs)
+        want_t, want_c = po.policy_act(y)
+        # a mismatch is allowed only where the reference sits on a rounding boundary
+        near = (np.abs(np.abs(y[:, 0] * 16 - np.floor(y[:, 0] * 16)) - 0.5) < 0.05) | \
+               (np.abs(np.abs(y[:, 1] * 16 - np.floor(y[:, 1] * 16)) - 0.5) < 0.05)
+        ok = (want_t == at[t]) & (want_c == ac[t])
+        assert (ok | near).all(), f"step {t}: {np.count_nonzero(~(ok | near))} actions off"
+        assert ok.mean() > 0.98
