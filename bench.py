@@ -183,10 +183,14 @@ def main():
             kms.append(eng.kernel_ms())
     elif cfg == 5:
         # back-to-back launches, one sync: the policy kernel is ~1 ms, and a
-        # host round trip per launch lets the shader clock sag between them
-        for _ in range(args.steps):
-            step_fn()
-        eng.sync()
+        # host round trip per launch lets the shader clock sag between them;
+        # an event pair around every launch gives the mean kernel duration
+        # (the figure rocprofv3's kernel trace averages)
+        avg, span = C.c_double(), C.c_double()
+        fn = eng.lib.ccka_debug_mlp_batch
+        fn.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        eng._chk(fn(eng.ctx, args.steps, C.byref(avg), C.byref(span)), "ccka_debug_mlp_batch")
+        kms = [avg.value]
     else:
         for _ in range(args.steps):
             step_fn()
@@ -194,8 +198,6 @@ def main():
             kms.append(eng.kernel_ms())
     barrier()
     elapsed = time.perf_counter() - t0
-    if cfg == 5 and not policy:  # per-launch average over the stream (launch gaps included: conservative)
-        kms = [elapsed * 1e3 / args.steps]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

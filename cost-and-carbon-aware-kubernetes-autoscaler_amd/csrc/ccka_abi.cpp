@@ -1481,6 +1481,55 @@ int ccka_mlp_forward_async(ccka_ctx* c) {
   return CCKA_OK;
 }
 
+// Internal measurement hook (bench.py config 5): `launches` back-to-back MLP
+// launches with an event pair around each one; *avg_ms = the mean kernel
+// duration (what rocprofv3 --kernel-trace averages), *span_ms = first start
+// to last end (launch gaps included).
+int ccka_debug_mlp_batch(ccka_ctx* c, int32_t launches, double* avg_ms, double* span_ms) {
+  if (!c || !avg_ms || !span_ms || launches < 1 || launches > 4096) return CCKA_EINVAL;
+  if (!c->mlp_have_w || !c->mlp_n) return fail(c, CCKA_ESTATE, "MLP weights / states not set");
+  (void)hipSetDevice(c->device);
+  std::vector<hipEvent_t> ev((size_t)launches * 2);
+  for (auto& e : ev) HIPCHK(c, hipEventCreate(&e));
+  MlpParams p{};
+  p.x = c->d_mx;
+  p.y = c->d_my;
+  p.w1f = c->d_w1f;
+  p.w2f = c->d_w2f;
+  p.w3f = c->d_w3f;
+  p.b1 = c->d_mb;
+  p.b2 = c->d_mb + MLP_HID;
+  p.b3 = c->d_mb + 2 * MLP_HID;
+  p.N = c->mlp_n;
+  p.stamps = nullptr;
+  int rc = CCKA_OK;
+  // the context's own pair spans the batch (ccka_sync / ccka_last_kernel_ms)
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
+  for (int k = 0; k < launches && rc == CCKA_OK; ++k) {
+    if (hipEventRecord(ev[2 * k], c->stream) != hipSuccess || launch_mlp(p, c->cus, c->stream) != hipSuccess ||
+        hipEventRecord(ev[2 * k + 1], c->stream) != hipSuccess)
+      rc = fail(c, CCKA_EHIP, "MLP batch launch %d", k);
+  }
+  double sum = 0.0;
+  float span = 0.f;
+  if (rc == CCKA_OK && hipEventRecord(c->ev1, c->stream) != hipSuccess) rc = fail(c, CCKA_EHIP, "event record");
+  if (rc == CCKA_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(c, CCKA_EHIP, "MLP batch sync");
+  for (int k = 0; k < launches && rc == CCKA_OK; ++k) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]) != hipSuccess) rc = fail(c, CCKA_EHIP, "event time");
+    sum += ms;
+  }
+  if (rc == CCKA_OK && hipEventElapsedTime(&span, ev[0], ev[2 * launches - 1]) != hipSuccess)
+    rc = fail(c, CCKA_EHIP, "event time");
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  if (rc != CCKA_OK) return rc;
+  *avg_ms = sum / launches;
+  *span_ms = span;
+  c->ran = true;
+  return CCKA_OK;
+}
+
 int ccka_mlp_forward(ccka_ctx* c) {
   int rc = ccka_mlp_forward_async(c);
   if (rc != CCKA_OK) return rc;

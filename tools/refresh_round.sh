@@ -12,7 +12,11 @@ for c in 2 3 4 5; do
   tools/gpu_step.sh bench_full_c$c 400 python bench.py --config $c || exit $?
   grep '^{' gpurun_out/bench_full_c$c.log | tail -1 > $out/bench_config$c.json || exit 1
 done
+tools/gpu_step.sh bench_full_c5p 400 python bench.py --config 5 --mode policy || exit $?
+grep '^{' gpurun_out/bench_full_c5p.log | tail -1 > $out/bench_config5_policy.json || exit 1
 tools/prof_round1.sh $out/p1 || exit $?
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$out/c5p/trace" -o run --output-format csv -- \
+  python3 bench.py --config 5 --mode policy --steps 2 --warmup 1 --no-cpu > "$out/c5p_trace.log" 2>&1 || exit $?
 tools/prof_issue.sh $out/issue || exit $?
 tools/prof_mlp.sh $out/mlp || exit $?
 echo refresh-done
