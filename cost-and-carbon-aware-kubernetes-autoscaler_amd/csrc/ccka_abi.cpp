@@ -242,8 +242,8 @@ static int d1_check_world(ccka_ctx* c) {
   c->d1_ready = false;
   const ccka_deployment& dp = w.deploy[0];
   if (w.n_deploy != 1 || dp.scaler != CCKA_SCALER_HPA) return CCKA_OK;
-  // drift / replacement run on the general kernel unless d1_prepare proves
-  // them inert for these scenarios (d1_disrupt_inert)
+  // replacement / multi-node consolidation run on the general kernel unless
+  // d1_prepare proves them inert for these scenarios (d1_disrupt_ok)
   for (int q = 0; q < w.n_pools; ++q)
     if (w.pools[q].limit_cpu_m >= 0 || w.pools[q].limit_mem_mi >= 0) return CCKA_OK;
   // one HPA decision per step over the 8-entry register rings
@@ -307,6 +307,7 @@ static int d1_check_world(ccka_ctx* c) {
   if ((rc = dupload(c, c->d_cap1s, cap1s.data(), cap1s.size())) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_zmasks, zm.data(), zm.size())) != CCKA_OK) return rc;
   c->zmasks = zm;
+  for (size_t z = 0; z < 16; ++z) p.zml[z] = z < zm.size() ? zm[z] : 0u;
   c->JT = jmax + 1;
   p.T = w.n_steps; p.K = K; p.Z = w.n_zones; p.R = w.n_regions; p.NP = w.n_pools; p.maxn = w.max_nodes;
   p.NZI = (int)zm.size(); p.JT = c->JT;
@@ -329,42 +330,48 @@ static int d1_check_world(ccka_ctx* c) {
   return CCKA_OK;
 }
 
-// The single-deployment kernel has no drift / replacement phases; it may run a
-// world that enables them only when they provably never act (exact):
-//  - drift needs a profile change that moves a pool's zone or capacity-type
-//    mask: never when no scenario switches, or OFFPEAK and PEAK resolve to the
-//    same masks for every pool;
-//  - replacement needs an on-demand node in a WhenEmptyOrUnderutilized pool:
-//    never when no pool profile uses that policy or no scenario's nodeSelector
-//    admits on-demand.
-static bool d1_disrupt_inert(const ccka_ctx* c) {
+// Drift never acts when no scenario switches profile or OFFPEAK and PEAK
+// resolve to the same masks for every pool.
+static bool d1_drift_inert(const ccka_ctx* c) {
   const ccka_world& w = c->hw;
-  if (w.disrupt_ext & CCKA_DISRUPT_DRIFT) {
-    const bool switching = c->sc_pswitch_any >= 0 ? c->sc_pswitch_any != 0 : w.peak_switch != 0;
-    bool same = true;
-    for (int q = 0; q < w.n_pools; ++q) {
-      uint32_t zm = 0, cm = 0;
-      for (const ccka_pool_patch* x : {&w.pools[q].base, &w.pools[q].profile[CCKA_PROFILE_RESET]}) {
-        if (x->zone_mask) zm = x->zone_mask;
-        if (x->cap_mask) cm = x->cap_mask;
-      }
-      // masks after the first profile (t = 0, either one) must never change
-      // over the alternations that follow (merge: 0 keeps the previous mask)
-      const ccka_pool_patch* pr[2] = {&w.pools[q].profile[CCKA_PROFILE_OFFPEAK],
-                                      &w.pools[q].profile[CCKA_PROFILE_PEAK]};
-      for (int first = 0; first < 2; ++first) {
-        uint32_t z = zm, k = cm, z1 = 0, k1 = 0;
-        for (int j = 0; j < 4; ++j) {
-          const ccka_pool_patch* x = pr[(first + j) & 1];
-          if (x->zone_mask) z = x->zone_mask;
-          if (x->cap_mask) k = x->cap_mask;
-          if (j == 0) { z1 = z; k1 = k; }
-          else if (z != z1 || k != k1) same = false;
-        }
+  if (!(w.disrupt_ext & CCKA_DISRUPT_DRIFT)) return true;
+  const bool switching = c->sc_pswitch_any >= 0 ? c->sc_pswitch_any != 0 : w.peak_switch != 0;
+  bool same = true;
+  for (int q = 0; q < w.n_pools; ++q) {
+    uint32_t zm = 0, cm = 0;
+    for (const ccka_pool_patch* x : {&w.pools[q].base, &w.pools[q].profile[CCKA_PROFILE_RESET]}) {
+      if (x->zone_mask) zm = x->zone_mask;
+      if (x->cap_mask) cm = x->cap_mask;
+    }
+    // masks after the first profile (t = 0, either one) must never change
+    // over the alternations that follow (merge: 0 keeps the previous mask)
+    const ccka_pool_patch* pr[2] = {&w.pools[q].profile[CCKA_PROFILE_OFFPEAK],
+                                    &w.pools[q].profile[CCKA_PROFILE_PEAK]};
+    for (int first = 0; first < 2; ++first) {
+      uint32_t z = zm, k = cm, z1 = 0, k1 = 0;
+      for (int j = 0; j < 4; ++j) {
+        const ccka_pool_patch* x = pr[(first + j) & 1];
+        if (x->zone_mask) z = x->zone_mask;
+        if (x->cap_mask) k = x->cap_mask;
+        if (j == 0) { z1 = z; k1 = k; }
+        else if (z != z1 || k != k1) same = false;
       }
     }
-    if (switching && !same) return false;
   }
+  return !switching || same;
+}
+
+// The single-deployment kernel runs drift itself (8 slots, <= 2 pools: its
+// DRIFT instantiation, SEMANTICS 3.G0); replacement and multi-node
+// consolidation run on the general kernel unless provably inert:
+//  - replacement needs an on-demand node in a WhenEmptyOrUnderutilized pool:
+//    never when no pool profile uses that policy or no scenario's nodeSelector
+//    admits on-demand;
+//  - multi-node consolidation needs a WhenEmptyOrUnderutilized pool.
+static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift) {
+  const ccka_world& w = c->hw;
+  *drift = !d1_drift_inert(c);
+  if (*drift && !(w.max_nodes <= 8 && w.n_pools <= 2)) return false;
   bool weou = false;
   for (int q = 0; q < w.n_pools; ++q) {
     weou |= w.pools[q].base.policy == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
@@ -374,7 +381,6 @@ static bool d1_disrupt_inert(const ccka_ctx* c) {
     const uint32_t sel = c->sc_capsel_or ? c->sc_capsel_or : w.deploy[0].cap_sel;
     if (weou && (sel & CCKA_CAP_OD)) return false;
   }
-  // multi-node consolidation needs a WhenEmptyOrUnderutilized pool
   if ((w.disrupt_ext & CCKA_DISRUPT_MULTI) && weou) return false;
   return true;
 }
@@ -383,7 +389,9 @@ static bool d1_disrupt_inert(const ccka_ctx* c) {
 static int d1_prepare(ccka_ctx* c) {
   c->d1_ready = true;
   c->d1_ok = false;
-  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_inert(c)) return CCKA_OK;
+  bool drift = false;
+  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_ok(c, &drift)) return CCKA_OK;
+  c->d1.drift = drift ? 1 : 0;
   if (c->sc_dstab_max > CCKA_HIST * CCKA_STEP_SECONDS) return CCKA_OK;  // beyond the register ring
   const size_t n = (size_t)c->N;
   std::vector<double> wl;

@@ -201,6 +201,8 @@ struct D1Params {
   D1Rule up, dn;
   int32_t budget[CCKA_MAX_POOLS];
   D1Patch patch[CCKA_MAX_POOLS][4];  // base, RESET, OFFPEAK, PEAK
+  int32_t drift;                     // 1: Karpenter drift (SEMANTICS 3.G0) in the kernel
+  uint32_t zml[16];                  // zone mask of each zone-mask index (patch zi)
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)

@@ -303,7 +303,7 @@ constexpr int D1_PF = D1_PF_OVERRIDE;
 #define D1_V_NU 1   // 1: the unready-pods utilisation only in lanes with unready pods
 #endif
 
-template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF>
+template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
@@ -409,6 +409,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0; sinv[n] = 0.f;
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
+  // DRIFT (SEMANTICS 3.G0): drifted slots, sources of an in-flight pre-spun
+  // replacement and those replacements (tainted karpenter.sh/disrupted: no
+  // pods placed on them, no consolidation; a replacement's source is
+  // 1 + slot in sinfo bits 16..20)
+  uint32_t dmask = 0, srcm = 0, repm = 0;
+  auto taint = [&]() -> uint32_t { return DRIFT ? (srcm | repm) : 0u; };
   const uint32_t slot_mask = maxn >= 32 ? 0xFFFFFFFFu : ((1u << maxn) - 1u);
 
   int replicas = p.replicas0, placed = 0, rpods = 0;
@@ -507,7 +513,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             rpods += spods[n];
             sallocr[n] = salloc[n];
             acc_dirty = true;
-            if (cmask >> n & 1u) Ffree += scap[n] - spods[n];
+            if ((cmask & ~taint()) >> n & 1u) Ffree += scap[n] - spods[n];
           }
           else next_ready = min(next_ready, sready[n]);
         }
@@ -538,6 +544,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           scas[n] = c;
         }
       refresh_J(rh);
+      if constexpr (DRIFT) {  // the pools' requirements moved: which nodes left them
+        uint32_t dm = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) {
+          const uint32_t x = sinfo[n];
+          uint32_t zm = 0, cm = 0;
+#pragma unroll
+          for (int q = 0; q < MAXP; ++q)
+            if ((int)(x >> 13 & 3u) == q) { zm = pzi[q] >= 0 ? p.zml[pzi[q]] : 0u; cm = pcm[q]; }
+          const bool drifted = !(zm >> (x >> 10 & 3u) & 1u) || !(cm & capbit1((int)(x >> 12 & 1u)));
+          dm |= ((used >> n & 1u) && drifted ? 1u : 0u) << n;
+        }
+        dmask = dm;
+      }
     }
 
     D1_STAMP(1);
@@ -655,7 +675,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           spods[n] -= k;
           excess -= k;
           removed += k;
-          if (pass == 1) removed_c += (cmask >> n & 1u) ? k : 0;
+          if (pass == 1) removed_c += ((cmask & ~taint()) >> n & 1u) ? k : 0;
           slc[n] = k > 0 ? t + scas[n] : slc[n];
         }
         if (pass == 1) { rpods -= removed; Ffree += removed_c; acc_dirty = acc_dirty || removed > 0; }
@@ -666,7 +686,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     if (pd > 0) {
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask;
+        const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask & ~taint();
         if (!m || pd <= 0) continue;  // skipped by the wave when no lane needs the pass
         int added = 0;
 #pragma unroll
@@ -772,14 +792,92 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) weou |= pmask[q];
     const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)));
     if constexpr (STAMPS) st_acc[10] += __ballot(gate != 0) != 0 ? 1 : 0;
-    if (gate && !(ablate & 1)) {
+    // DRIFT: ready replacements take over (G1); drifted ready nodes not yet
+    // being replaced are drift candidates (G0)
+    const uint32_t tkm = DRIFT ? (repm & rdy) : 0u;
+    const uint32_t dwork = DRIFT ? (dmask & rdy & ~srcm) : 0u;
+    if ((gate || tkm || dwork) && !(ablate & 1)) {
+      bool any_del = false;
+      // free capacity of the compatible ready untainted slots, from scratch
+      auto ffree_now = [&]() {
+        int f = 0;
+        const uint32_t m = rdy & cmask & ~taint();
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n) f += (m >> n & 1u) ? scap[n] - spods[n] : 0;
+        Ffree = f;
+      };
+      auto masks_now = [&]() {
+        uint32_t el = 0, em = 0;
+#pragma unroll
+        for (int n = MAXN - 1; n >= 0; --n) {
+          el = 2 * el + (slc[n] <= t ? 1u : 0u);
+          em = 2 * em + (spods[n] == 0 ? 1u : 0u);
+        }
+        elig = el & rdy;
+        emp = em & used;
+      };
+      // a slot leaves the cluster (its pods are gone or moved already)
+      auto drop_slot = [&](int b) {
+        uint32_t binfo = 0;
+        int bprice = 0;
+#pragma unroll
+        for (int n = 0; n < MAXN; ++n)
+          if (n == b) {
+            binfo = sinfo[n];
+            bprice = sprice[n];
+            sallocr[n] = 0;
+            spods[n] = 0;
+            sinfo[n] = 0;
+          }
+        if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
+        burn -= bprice;
+        const int4 ac = s_acc[binfo & 1023u];
+        Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
+        const uint32_t nb = ~(1u << b);
+        used &= nb; rdy &= nb; cmask &= nb; dmask &= nb; srcm &= nb; repm &= nb;
+#pragma unroll
+        for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
+        deletions++;
+        any_del = true;
+        acc_dirty = true;
+      };
+      if constexpr (DRIFT) {
+        if (tkm) {
+          // G1: each ready replacement (slot order) takes its source's pods up
+          // to its free capacity; the rest are evicted; the source is deleted
+          uint32_t tk = tkm;
+          while (tk) {
+            const int m = __ffs((int)tk) - 1;
+            tk &= tk - 1;
+            uint32_t xm = 0;
+            int capm = 0, podm = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n)
+              if (n == m) { xm = sinfo[n]; sinfo[n] = xm & 0xFFFFu; capm = scap[n]; podm = spods[n]; }
+            const int src = (int)(xm >> 16 & 31u) - 1;
+            int sp = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) sp = n == src ? spods[n] : sp;
+            const int k = (capbit1((int)(xm >> 12 & 1u)) & capsel) ? min(capm - podm, sp) : 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n)
+              if (n == m) { spods[n] += k; slc[n] = t + scas[n]; }
+            rpods -= sp - k;
+            placed -= sp - k;
+            repm &= ~(1u << m);
+            drop_slot(src);
+            flags |= 4u;
+          }
+          ffree_now();
+          masks_now();
+        }
+      }
       // PDB evictions allowed (32-bit: pct <= 100 and replicas <= 32767)
       int allowed = 0x7fffffff;
       if (pdb_pct >= 0) {
         const int rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
         allowed = max(rdyp - (int)(((uint32_t)(pdb_pct * reps) + 99u) / 100u), 0);
       }
-      bool any_del = false;
 #pragma unroll
       for (int q = 0; q < MAXP; ++q) {
         if (q >= NP) break;
@@ -788,8 +886,105 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         const int qbudget = (budget[q] * npool + 99) / 100;
         const bool weou_q = ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
         int deleted = 0;
+        if constexpr (DRIFT) {
+          // G0: drifted ready nodes of the pool in slot order, sharing its budget
+          uint32_t dc = dmask & rdy & ~srcm & pmask[q];
+          bool acted = false;
+          while (dc && deleted < qbudget) {
+            const int best = __ffs((int)dc) - 1;
+            dc &= dc - 1;
+            int bp = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) bp = n == best ? spods[n] : bp;
+            const int pdbp = pdb_member ? bp : 0;
+            if (pdbp > allowed) continue;
+            acted = true;
+            // pods move first-fit onto ready, non-drifted, untainted compatible nodes
+            const uint32_t recv = rdy & ~dmask & ~taint() & cmask;
+            int need = bp;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
+              const int k = min(fr, need);
+              spods[n] += k;
+              need -= k;
+              slc[n] = k > 0 ? t + scas[n] : slc[n];
+            }
+            // the rest: a pre-spun replacement under the pool's current
+            // requirements (the F launch rule: the argmin table row), else eviction
+            const uint32_t fr = ~used & slot_mask;
+            int2 e = make_int2(0, -1);
+            uint32_t cmq = 0;
+            int cq = 0;
+            if (need > 0 && fr) {
+              int J = 0, zq = -1;
+#pragma unroll
+              for (int qq = 0; qq < MAXP; ++qq)
+                if (qq == q) { J = pJ[qq]; zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
+              if (cmq && zq >= 0 && need <= J)
+                e = *(const int2*)(table + ((((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * NW + wi) * JT + need);
+            }
+            if (e.y >= 0 && need > 0) {
+              const int info = e.y, price = e.x;
+              const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
+              const int slot = __ffs((int)fr) - 1;
+              const int rs = t + delay;
+              const int4 ac = s_acc[bk];
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                if (n == slot) {
+                  sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13 | (best + 1) << 16);
+                  sready[n] = rs;
+                  slc[n] = t + casc(cq);
+                  scas[n] = casc(cq);
+                  spods[n] = 0;
+                  sprice[n] = price;
+                  scap[n] = cap1;
+                  sdyn[n] = (uint32_t)ac.z;
+                  salloc[n] = ac.w;
+                  sallocr[n] = delay == 0 ? ac.w : 0;
+                  sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
+                }
+                if (n == best) spods[n] = need;
+              }
+              const uint32_t bit = 1u << slot;
+              used |= bit;
+              if (capbit1(bc) & capsel) cmask |= bit;
+#pragma unroll
+              for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
+              if (delay == 0) {
+                rdy |= bit;
+                acc_dirty = true;
+              } else {
+                next_ready = min(next_ready, rs);
+              }
+              minscap = min(minscap, cap1);
+              Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
+              if (bc == 0) nsp++; else nod++;
+              burn += price;
+              launches++;
+              last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+              hash = (hash ^ last_choice) * 16777619u;
+              step_last_type = bk;
+              srcm |= 1u << best;
+              repm |= bit;
+              flags |= 2u | 16u | 32u;
+            } else {
+              rpods -= need;
+              placed -= need;
+              drop_slot(best);
+              flags |= 4u | 16u;
+            }
+            allowed -= pdbp;
+            deleted++;
+          }
+          if (acted) {
+            ffree_now();
+            masks_now();
+          }
+        }
         while (deleted < qbudget) {
-          const uint32_t cand = elig & pmask[q];
+          const uint32_t cand = elig & pmask[q] & ~taint();
           const uint32_t ce = cand & emp;
           if (!ce && !(weou_q && (cand & ~emp) && (Ffree >= minscap || (cand & ~emp & ~cmask)))) break;
           int best = -1, bpods = 0, bprice = -1, bcap = 0;
@@ -828,7 +1023,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               bprice = 0x7fffffff - (int)((bkey >> 4) & 0x7fffffffull);
               // move its pods first-fit onto the other compatible ready nodes
               int need = bpods;
-              const uint32_t recv = rdy & cmask & ~(1u << best);
+              const uint32_t recv = rdy & cmask & ~(1u << best) & ~taint();
 #pragma unroll
               for (int n = 0; n < MAXN; ++n) {
                 const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
@@ -854,6 +1049,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           Ffree -= ((rdy & cmask) >> best & 1u) ? bcap : bpods;
           const uint32_t nb = ~(1u << best);
           used &= nb; rdy &= nb; cmask &= nb;
+          if constexpr (DRIFT) dmask &= nb;
 #pragma unroll
           for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
           if (pdb_member) allowed -= bpods;
@@ -989,7 +1185,10 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const size_t lds = (size_t)p.K * sizeof(int4);
   // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
-  if (p.stamps) {
+  if (p.drift) {  // drift (SEMANTICS 3.G0): 8 slots, <= 2 pools (d1_disrupt_ok)
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true>), dim3(grid), dim3(B), lds, s, p);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true>), dim3(grid), dim3(B), lds, s, p);
+  } else if (p.stamps) {
     if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, p);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, false>), dim3(grid), dim3(B), lds, s, p);
   } else if (p.maxn <= 8 && p.NP <= 2 && p.occ == 3) {

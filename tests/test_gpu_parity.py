@@ -275,6 +275,36 @@ def test_d1_matches_general_kernel(engine):
     compare(r2, r1, t2, t1)
 
 
+@pytest.mark.parametrize("variant", ["drift", "drift_pdb_budget", "drift_delay0_bdef"])
+def test_d1_drift_matches_general_kernel(engine, variant):
+    """The single-deployment kernel's drift (pre-spun replacements, takeovers,
+    taint) against the general kernel on the same inputs, bit for bit."""
+    spec = configs.config2_world(n_steps=1440)
+    spec.drift = 1
+    n = 2222
+    sc = configs.hpa_scenarios(n, first_id=7)
+    if variant == "drift_pdb_budget":
+        spec.pdb_pct = 80
+        for p in spec.pools:
+            p.budget_pct = 40
+    elif variant == "drift_delay0_bdef":
+        spec.provision_delay_steps = 0
+        spec.pdb_pct = -1
+        sc.down_stab_s = np.full(n, 120, np.int16)
+    load = po.gen_load(configs.trace_gen(2), spec.n_steps, 1, n, first_id=7)
+    r2, t2 = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    engine.set_engine(1)
+    try:
+        engine.rollout(trajectory=True)
+        assert engine.last_engine()[0] == 1
+        r1, t1 = engine.results(), engine.trajectory()
+    finally:
+        engine.set_engine(0)
+    assert ((t1["flags"] & 48) == 48).any() and ((t1["flags"] & 20) == 20).any()
+    compare(r2, r1, t2, t1)
+
+
 # ---------------------------------------------------------------------------
 # Karpenter drift on the peak/off-peak zone switch (SEMANTICS 3.G0, SURVEY 8(f)-1)
 # ---------------------------------------------------------------------------
@@ -307,7 +337,9 @@ def test_drift_parity_single_deployment(engine, variant):
         spec.pdb_pct = -1
     load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=sc.first_id)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
-    assert engine.last_engine()[0] == 1  # drift runs on the general kernel
+    # drift runs inside the single-deployment kernel (8 slots, no pool limits),
+    # otherwise on the general kernel
+    assert engine.last_engine()[0] == (1 if variant in ("pool_limit", "slots16") else 2), variant
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
     f = tc["flags"]
     # both drift branches are covered: a pre-spun replacement (flags 16|32) where
@@ -434,7 +466,7 @@ def test_inert_disruption_runs_on_d1(engine):
     """Worlds that enable drift / replacement where neither can ever act run on
     the single-deployment kernel and still match the oracle (which runs the
     phases); a world where they can act runs on the general kernel."""
-    spec = configs.config2_world(n_steps=720)
+    spec = configs.config2_world(n_steps=1440)
     spec.replace = 1
     sc = configs.hpa_scenarios(1200)
     run_engine(engine, spec, sc, load=po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n))
@@ -445,10 +477,17 @@ def test_inert_disruption_runs_on_d1(engine):
     assert engine.last_engine()[0] == 2
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
     compare(rg, rc, tg, tc)
-    spec.drift = 1  # zones move at the switch: drift can act
-    run_engine(engine, spec, sc, load=load)
+    spec.drift = 1  # zones move at the switch: drift acts, inside the single-deployment kernel
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert (tc["flags"] & 16).any()
+    compare(rg, rc, tg, tc)
+    spec.max_nodes = 12  # beyond its 8 slots: the general kernel
+    run_engine(engine, spec, sc, load=po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n))
     assert engine.last_engine()[0] == 1
-    sc.peak_switch = np.zeros(sc.n, np.uint8)  # ... unless no scenario switches
+    spec.max_nodes = 8
+    sc.peak_switch = np.zeros(sc.n, np.uint8)  # no scenario switches: drift is inert
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
     assert engine.last_engine()[0] == 2
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
