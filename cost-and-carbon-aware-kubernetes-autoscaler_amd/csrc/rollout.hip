@@ -246,7 +246,6 @@ __device__ __forceinline__ int util_div(long long usage, long long den) {
 struct Rule {
   int sel, n, stab_mask;
   int type[2], value[2], pmask[2];
-  double factor[2];  // Percent: 1 +/- value/100 (computed exactly as the spec writes it)
 };
 
 // Hot deployment fields, hoisted out of the step loop into registers. Loaded
@@ -277,7 +276,6 @@ __device__ __forceinline__ Rule load_rule(const ccka_hpa_rules* r, bool up) {
     o.type[q] = r->policies[q].type;
     o.value[q] = r->policies[q].value;
     o.pmask[q] = window_mask(r->policies[q].period_s);
-    o.factor[q] = up ? (1.0 + (double)o.value[q] / 100.0) : (1.0 - (double)o.value[q] / 100.0);
   }
   return o;
 }
@@ -320,8 +318,10 @@ __device__ __forceinline__ int rate_limit(const Rule& R, bool up, int cur, const
     const long long pst = (long long)cur - added + removed;
     long long pr;
     if (R.type[q] == CCKA_HPA_PODS) pr = up ? pst + R.value[q] : pst - R.value[q];
-    else if (up) pr = (int)ceil((double)pst * R.factor[q]);
-    else pr = (int)((double)pst * R.factor[q]);
+    // Percent: 1 +/- value/100 computed exactly as the spec writes it (on use:
+    // rare, and no registers held across the step loop)
+    else if (up) pr = (int)ceil((double)pst * (1.0 + (double)R.value[q] / 100.0));
+    else pr = (int)((double)pst * (1.0 - (double)R.value[q] / 100.0));
     res = (up == min_sel) ? min(res, pr) : max(res, pr);
   }
   return (int)res;
@@ -425,7 +425,7 @@ __device__ int behavior_long(const ccka_hpa_rules* up, const ccka_hpa_rules* dn,
 }
 
 template <int DMAX, int MAXN>
-__global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
+__global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout_kernel(KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // world through the constant address space for rare (profile-switch) reads;
   // hot fields are hoisted into registers below
@@ -448,14 +448,20 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
   double* s_ci = reinterpret_cast<double*>(smem + p.lds_off_ci);  // [span][24][gpwmin, gpwh]
 
   // ---- stage the catalog, the region range of this block ----
+  static_assert(sizeof(ccka_itype) == 48, "catalog entries are staged as three 16-byte words");
   for (int k = tid; k < K; k += blockDim.x) {
-    const ccka_itype ty = p.types[k];
-    L.types[k] = ty;
-    if (DMAX == 1) {
+    // three 16-byte words (a struct copy would go through a private temporary)
+    const int4* src = reinterpret_cast<const int4*>(p.types + k);
+    const int4 a = src[0], b = src[1], c = src[2];
+    int4* dst = reinterpret_cast<int4*>(L.types + k);
+    dst[0] = a;
+    dst[1] = b;
+    dst[2] = c;
+    if (DMAX == 1) {  // vcpu, alloc_cpu_m, alloc_mem_mi, max_pods are the first word
       const int rc = w->deploy[0].req_cpu_m, rm = w->deploy[0].req_mem_mi;
-      int f = ty.max_pods;
-      if (rc > 0) f = min(f, ty.alloc_cpu_m / rc);
-      if (rm > 0) f = min(f, ty.alloc_mem_mi / rm);
+      int f = a.w;
+      if (rc > 0) f = min(f, a.y / rc);
+      if (rm > 0) f = min(f, a.z / rm);
       L.cap1[k] = f;
     }
   }
@@ -790,7 +796,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
         g_dirty = true;
 #pragma unroll
         for (int q = 0; q < CCKA_MAX_POOLS; ++q) {
-          if (q >= NP) break;
+          if (q >= NP) continue;
           auto& x = w->pools[q].profile[prof];
           if (x.policy != CCKA_POLICY_KEEP) ppol[q] = x.policy;
           if (x.consolidate_after_s >= 0) pca[q] = x.consolidate_after_s;
@@ -806,7 +812,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       }
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        if (d >= D) break;
+        if (d >= D) continue;
         const Dep& dp = dep[d];
         const int Lv = Lcur[d];
         if (dp.scaler != CCKA_SCALER_HPA && dp.scaler != CCKA_SCALER_KEDA) continue;  // static / trigger
@@ -925,7 +931,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        if (d >= D) break;
+        if (d >= D) continue;
         int excess = placed[d] - replicas[d];
         if (excess > 0) {
           g_dirty = true;
@@ -950,9 +956,11 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
       // nodes tainted karpenter.sh/disrupted (a source whose pre-spun
       // replacement is in flight, and that replacement) take no other pods
       const uint32_t tnt = (greplace || gdrift || gmulti) ? taint_mask() : 0u;
-#pragma unroll
+      // (a 16-deployment body is too large to unroll: the loop stays rolled there)
+      constexpr int kUnrollE = DMAX <= 4 ? DMAX : 1;
+#pragma unroll kUnrollE
       for (int d = 0; d < DMAX; ++d) {
-        if (d >= D) break;
+        if (d >= D) continue;
         int pd = replicas[d] - placed[d];
         if (pd > 0) {
 #pragma unroll
@@ -969,7 +977,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                   int sc = 0, sm = 0, sp = 0;
 #pragma unroll
                   for (int e = 0; e < DMAX; ++e) {
-                    if (e >= D) break;
+                    if (e >= D) continue;
                     sc += npods[n][e] * dep[e].req_cpu;
                     sm += npods[n][e] * dep[e].req_mem;
                     sp += npods[n][e];
@@ -1395,7 +1403,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               }
 #pragma unroll
               for (int d = 0; d < DMAX; ++d) {
-                if (d >= D) break;
+                if (d >= D) continue;
                 int need_d = cp[d];
 #pragma unroll
                 for (int m = 0; m < MAXN; ++m) {
@@ -1408,7 +1416,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                       int sc = 0, sm = 0, sp = 0;
 #pragma unroll
                       for (int e = 0; e < DMAX; ++e) {
-                        if (e >= D) break;
+                        if (e >= D) continue;
                         sc += tpods[m][e] * dep[e].req_cpu;
                         sm += tpods[m][e] * dep[e].req_mem;
                         sp += tpods[m][e];
@@ -1523,7 +1531,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
               }
 #pragma unroll
               for (int d = 0; d < DMAX; ++d) {
-                if (d >= D) break;
+                if (d >= D) continue;
                 int k = 0;
                 if (capbit(ni_cap(xm)) & capsel[d]) {
 #pragma unroll
@@ -1536,7 +1544,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                         int sc = 0, smm = 0, spp = 0;
 #pragma unroll
                         for (int e = 0; e < DMAX; ++e) {
-                          if (e >= D) break;
+                          if (e >= D) continue;
                           sc += npods[n][e] * dep[e].req_cpu;
                           smm += npods[n][e] * dep[e].req_mem;
                           spp += npods[n][e];
@@ -1637,7 +1645,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                       int sc = 0, sm = 0, sp = 0;
 #pragma unroll
                       for (int e = 0; e < DMAX; ++e) {
-                        if (e >= D) break;
+                        if (e >= D) continue;
                         sc += npods[n][e] * dep[e].req_cpu;
                         sm += npods[n][e] * dep[e].req_mem;
                         sp += npods[n][e];
@@ -1842,7 +1850,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                 if (pdb_pods > allowed) ok = false;
 #pragma unroll
                 for (int d = 0; d < DMAX; ++d) {
-                  if (d >= D || !ok) break;
+                  if (d >= D || !ok) continue;
                   int need_d = bp[d];
 #pragma unroll
                   for (int n = 0; n < MAXN; ++n) {
@@ -1851,7 +1859,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(KParams p) {
                       int sc = 0, sm = 0, sp = 0;
 #pragma unroll
                       for (int e = 0; e < DMAX; ++e) {
-                        if (e >= D) break;
+                        if (e >= D) continue;
                         sc += tpods[n][e] * dep[e].req_cpu;
                         sm += tpods[n][e] * dep[e].req_mem;
                         sp += tpods[n][e];
