@@ -494,7 +494,12 @@ def cpu_baseline_mlp(target_s):
 
     from ccka import configs
 
-    threads = max(1, len(os.sched_getaffinity(0)))
+    cpu = host_cpu()
+    # the rollout baseline's rule: affinity capped by the cgroup CPU quota
+    # (256 threads on a 16-CPU quota only time-slice the GEMMs)
+    threads = max(1, cpu["affinity"])
+    if cpu["cgroup_cpus"]:
+        threads = max(1, min(threads, int(cpu["cgroup_cpus"])))
     torch.set_num_threads(threads)
     ws, bs = configs.mlp_weights(11)
     w = [torch.from_numpy(configs.from_bf16_bits(configs.to_bf16_bits(x))) for x in ws]
@@ -515,7 +520,8 @@ def cpu_baseline_mlp(target_s):
     times.sort()
     med = times[len(times) // 2]
     return {"value": n / med, "unit": "cluster-states/s", "cores": threads, "kind": "port",
-            "sample": f"{n} states, PyTorch fp32 (bf16-rounded activations), median of {len(times)} runs"}
+            "sample": f"{n} states, PyTorch fp32 (bf16-rounded activations), median of {len(times)} runs",
+            "nproc": cpu["nproc"], "cpu_model": cpu["cpu_model"], "cgroup_cpus": cpu["cgroup_cpus"]}
 
 
 if __name__ == "__main__":
