@@ -284,30 +284,74 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
     st_last = now_;                                          \
   }
 
-// Load samples are prefetched PF steps ahead (a register FIFO): a step now
-// takes well under an HBM miss, and every in-step vector-memory wait (the
-// argmin-table row of a launch, the hourly price tile) also waits for all
-// older loads still in flight.
-#ifndef D1_PF_OVERRIDE
-constexpr int D1_PF = 3;
-#else
-constexpr int D1_PF = D1_PF_OVERRIDE;
+// ---------------------------------------------------------------------------
+// Lane-skewed schedule (docs/DESIGN.md "rollout_d1_kernel"):
+// every lane (scenario) keeps its own step counter. Most lane-steps are
+// quiet: the HPA keeps the replica count (desired == current, including the
+// steps the stabilisation window or maxReplicas hold it) and no node becomes
+// ready, no hour / profile boundary is crossed and no node becomes a new
+// consolidation candidate. A quiet step is the HPA evaluation, the history
+// push, the step's energy from cached sums and the trajectory record. Any
+// other step is an event: the lane stalls and the wave runs the full step
+// for all stalled lanes together every D1_K iterations, so the long event
+// path runs once for many lanes instead of once per step for the union of
+// every lane's events. Per-step constants (node cost, idle energy, pending
+// pods, node-minutes) are added lazily at the next event.
+//
+// Load samples reach the lanes through a per-wave LDS ring of D1_RB trace
+// rows (row t, lane l at [t % D1_RB][l]) filled by LDS-DMA
+// (global_load_lds_dword, one row = the wave's scenarios at one step) D1_K
+// rows every D1_K iterations, far ahead of the lanes; a row is read only
+// after D1_VMN younger DMA instructions were issued and `s_waitcnt
+// vmcnt(D1_VMN)` retired it (every DMA instruction is one consecutive row).
+// The ring is refilled only when every live lane has consumed the rows it
+// overwrites.
+// ---------------------------------------------------------------------------
+// (build-time overrides for tools/build_variants.py; the shipped build uses the defaults)
+#ifndef D1_RB_V
+#define D1_RB_V 64
 #endif
+#ifndef D1_K_V
+#define D1_K_V 8
+#endif
+#ifndef D1_VMN_V
+#define D1_VMN_V 24
+#endif
+#ifndef D1_LEAN_V
+#define D1_LEAN_V 1
+#endif
+#ifndef D1_LAG_V
+#define D1_LAG_V 0
+#endif
+constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
+constexpr int D1_K = D1_K_V;      // event cadence and DMA batch (iterations, power of two)
+constexpr int D1_VMN = D1_VMN_V;  // rows in flight (vmcnt bound; <= 63)
+static_assert(D1_VMN + 2 * D1_K < D1_RB, "ring too small for the DMA lead");
+constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
 
-// build-time variants of the single-deployment kernel (tools/variants.sh
-// compares them; the shipped build uses the defaults)
-#ifndef D1_V_ACC
-#define D1_V_ACC 0  // 0: per-node exact energy every step; 1: cached sums refreshed on change
-#endif
-#ifndef D1_V_NU
-#define D1_V_NU 1   // 1: the unready-pods utilisation only in lanes with unready pods
-#endif
+__device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_row)
+      : "memory");
+}
+__device__ __forceinline__ void d1_wait_rows() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN) : "memory");
+}
+__device__ __forceinline__ void d1_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-  // per instance type: {idle_nw lo, idle_nw hi, dyn_nw_per_m, alloc_cpu_m} (one ds_read_b128)
+  // LDS: per instance type {idle_nw lo, idle_nw hi, dyn_nw_per_m, alloc_cpu_m}
+  // (one ds_read_b128), then the load-sample rings of the block's waves
   extern __shared__ __attribute__((aligned(16))) int4 s_acc[];
   for (int x = threadIdx.x; x < p.K; x += blockDim.x) {
     const long long idle = p.acc[x * 3 + 0];
@@ -318,7 +362,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t wv = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
   const int64_t i = wv * p.lpw + lane;
-  if (lane >= p.lpw || i >= p.N) return;  // no cross-lane operations below
+  if (lane >= p.lpw || i >= p.N) return;  // no cross-lane operations below but ballots
 
   // ---- per-scenario parameters ----
   const int r = p.region ? (int)p.region[i] : 0;
@@ -343,7 +387,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int pdb_pct = opq(p.pdb_pct), slo_util = opq(p.slo_util), delay = opq(p.delay);
   const int base_nodes = opq(p.base_nodes), base_type = opq(p.base_type);
   const int K = opq(p.K), Z = opq(p.Z), T = opq(p.T);
-  const int ps = opq(p.peak_start), pe = opq(p.peak_end);
+  const int ps = opq(p.peak_start) % 1440, pe = opq(p.peak_end) % 1440;
+  const int ps_raw = opq(p.peak_start), pe_raw = opq(p.peak_end);
+  const int sm0 = opq(p.start_minute) % 1440;
   const long long base_nw = opq(p.base_nw), ls = opq(p.N);
   const GLOBAL_AS int32_t* const price = opq_ptr(p.price);
   const GLOBAL_AS double* const ci_gpwmin = opq_ptr(p.ci_gpwmin);
@@ -402,7 +448,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
   int salloc[MAXN];     // alloc_cpu_m of the slot's type (< 2^24 by eligibility)
   int sallocr[MAXN];    // salloc once the node is ready, else 0
-  float sinv[MAXN];     // 1/alloc (saturation pre-test of D1_V_ACC 1)
+  float sinv[MAXN];     // 1/alloc (saturation pre-test of the quiet step's energy)
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
     sinfo[n] = 0; sready[n] = 0; slc[n] = 0; scas[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
@@ -440,12 +486,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   long long cost = 0, burn = 0, base_price = 0;
   int pend_min = 0;  // <= 32767 pods x T steps
   long long energy_nw = 0, e_hour = 0, Isum = 0;  // exact nanowatt-minutes; Isum: idle draw of used slots
-  unsigned long long Ssum = 0;  // D1_V_ACC 1: sum over ready slots of dyn_nw_per_m * pods
-  float Rmax = 0.f;             // D1_V_ACC 1: max over ready slots of pods/alloc
-  bool acc_dirty = false;
   double gco2 = 0.0, ci_min = 0.0;
   int slo = 0, nmin_spot = 0, nmin_od = 0, launches = 0, deletions = 0, peak_nodes = 0;
   uint32_t last_choice = 0xFFFFFFFFu, hash = 2166136261u;
+
+  // quiet-step caches, refreshed at the end of every event step
+  unsigned long long Ssum = 0;  // sum over ready slots of dyn_nw_per_m * pods
+  float Rmax = 0.f;             // max over ready slots of pods/alloc
+  float q_rbd = 0.f, q_rbc = 0.f, q_rbp = 0.f;  // 1/(ready*req), 1/(cur*req), 1/ready pods
+  bool q_peak = false;
+  int q_rcap = 0, q_dreq = 1, q_dcur = 1;  // usage cap (ready*limit, or INT_MAX without a limit), ready*req, cur*req
+  int q_mode = 2;               // 0: metric (ready*req < 2^24), 1: no metric and replicas in range, 2: events only
+  bool q_unr = false;           // unready pods
+  int q_hit = -0x40000000;      // last step whose recorded proposal >= cur (down window hold)
+  const int wl = __popc(dnmask);  // down window: the last wl records
 
   auto refresh_J = [&](int rh) {
 #pragma unroll
@@ -455,124 +509,24 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
   };
 
-  // load column: the scenario's own trace, or its shared trace (policy sweeps)
-  const int32_t* lp = p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
-  const long long lsl = opq(p.NL);
-  // Memory pipeline of one step: at its top the previous step's trajectory
-  // record is stored and the load sample D1_PF steps ahead is issued; a sample
-  // enters the FIFO only at the end of its issuing step (opqv), so every wait
-  // the compiler places covers operations at least a step old.
-  int Lq[D1_PF];
-#pragma unroll
-  for (int k = 0; k < D1_PF; ++k) Lq[k] = opqv(lp[(int64_t)min(k, T - 1) * lsl]);
-  int4 rec_prev = make_int4(0, 0, 0, 0);
-  int minute = p.start_minute % 1440;
-
-  for (int t = 0; t < T; ++t, minute = minute == 1439 ? 0 : minute + 1) {
-    if (traj && t > 0) *(int4*)(traj + (int64_t)(t - 1) * ls + i) = rec_prev;
-    const int Lraw = lp[(int64_t)min(t + D1_PF, T - 1) * lsl];
-    const int L = Lq[0];
-    const int h = minute / 60;
-    const int rh = r * 24 + h;
-    if (h != hour) {  // wave-uniform: this hour's prices and carbon intensity
-      if (hour >= 0) gco2 += (double)e_hour * (ci_min * 1e-9);  // carbon of the hour that ended
-      e_hour = 0;
-      hour = h;
-      const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
-      ci_min = ci_gpwmin[rh];
-      base_price = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
-      burn = 0;
-      // every slot's price in flight at once (unused slots read entry 0)
-      int np[MAXN];
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        const uint32_t x = sinfo[n];
-        np[n] = tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
-      }
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        if (used >> n & 1u) {
-          sprice[n] = np[n];
-          burn += np[n];
-        }
-      }
-      refresh_J(rh);
-    }
-    uint32_t flags = 0;
-    int step_last_type = 0xFFFF;
-
-    D1_STAMP(0);
-    // ---- B. readiness ----
-    if (t >= next_ready) {
-      next_ready = 0x7fffffff;
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        if ((used & ~rdy) >> n & 1u) {
-          if (sready[n] <= t) {
-            rdy |= 1u << n;
-            rpods += spods[n];
-            sallocr[n] = salloc[n];
-            acc_dirty = true;
-            if ((cmask & ~taint()) >> n & 1u) Ffree += scap[n] - spods[n];
-          }
-          else next_ready = min(next_ready, sready[n]);
-        }
-      }
-    }
-    // ---- A. profile ----
-    const bool in_win = ps <= pe ? (minute >= ps && minute < pe) : (minute >= ps || minute < pe);
-    const bool peak = pswitch && in_win;
-    const int prof = peak ? CCKA_PROFILE_PEAK : CCKA_PROFILE_OFFPEAK;
-    if (peak) flags |= 1u;
-    if (prof != profile) {
-      profile = prof;
-#pragma unroll
-      for (int q = 0; q < MAXP; ++q) {
-        if (q >= NP) break;
-        const D1Patch& x = p.patch[q][prof + 1];
-        if (x.policy) ppol[q] = x.policy;
-        if (x.cas >= 0) pcas[q] = x.cas;
-        if (x.zi >= 0) pzi[q] = x.zi;
-        if (x.cm) pcm[q] = (uint32_t)x.cm;
-      }
-      // consolidateAfter may have changed: per-slot copies and thresholds
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n)
-        if (used >> n & 1u) {
-          const int c = casc(cas_of(sinfo[n]));
-          slc[n] += c - scas[n];
-          scas[n] = c;
-        }
-      refresh_J(rh);
-      if constexpr (DRIFT) {  // the pools' requirements moved: which nodes left them
-        uint32_t dm = 0;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) {
-          const uint32_t x = sinfo[n];
-          uint32_t zm = 0, cm = 0;
-#pragma unroll
-          for (int q = 0; q < MAXP; ++q)
-            if ((int)(x >> 13 & 3u) == q) { zm = pzi[q] >= 0 ? p.zml[pzi[q]] : 0u; cm = pcm[q]; }
-          const bool drifted = !(zm >> (x >> 10 & 3u) & 1u) || !(cm & capbit1((int)(x >> 12 & 1u)));
-          dm |= ((used >> n & 1u) && drifted ? 1u : 0u) << n;
-        }
-        dmask = dm;
-      }
-    }
-
-    D1_STAMP(1);
-    // ---- C. HPA (replica_calculator.go + horizontal.go, SEMANTICS §3.C) ----
-    // Straight-line in every lane (some lane of a wave has a scale event on
-    // nearly every step, so branches would only add exec-mask traffic).
-    // util = int32(usage*100 / (ready*req)) by an f32-reciprocal division with
-    // an exact remainder correction; the tolerance band, the unready rule and
-    // the SLO threshold are integer tests on util (exactly the binary64 tests
-    // of the spec, see ulo/uhi). The proposal ceil(fl(fl(u/target)*base))
-    // equals the exact integer ceiling unless u*base is a multiple of target
-    // (|rounding error| < 1/target otherwise); only that case, and inputs
-    // beyond the fast arithmetic's range, run the spec's expression (rare
-    // branches).
-    const int cur = replicas, ready = rpods;
+  // ---- C. HPA (replica_calculator.go + horizontal.go, SEMANTICS §3.C) ----
+  // Evaluated without side effects (the history push is hpa_commit):
+  // util = int32(usage*100 / (ready*req)) by an f32-reciprocal division with
+  // an exact remainder correction; the tolerance band, the unready rule and
+  // the SLO threshold are integer tests on util (exactly the binary64 tests
+  // of the spec, see ulo/uhi). The proposal ceil(fl(fl(u/target)*base))
+  // equals the exact integer ceiling unless u*base is a multiple of target
+  // (|rounding error| < 1/target otherwise); only that case, and inputs
+  // beyond the fast arithmetic's range, run the spec's expression (rare
+  // branches). Then the stabilisation (packed min / max over the records
+  // inside each window) and the rate limits; desired == cur exactly when
+  // proposal == cur.
+  struct HpaOut {
+    int util, proposal, desired;
+    bool ran, hpa_path;
+  };
+  auto hpa_eval = [&](int L, int cur, int ready, float rbd, float rbc) -> HpaOut {
+    HpaOut o;
     const bool metric = cur <= mx && cur >= minr && ready > 0 && !(cur == 0 && minr != 0);
     int util = 0, proposal = cur;
     {
@@ -582,13 +536,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       const int dreq = ready * req;     // < 2^31: ready <= 32767, req <= 65535
       const int dcur = cur * req;
       bool slow = usage < 0 || usage > 21474836;
-      util = fdiv_nb(a, dreq, __builtin_amdgcn_rcpf((float)dreq), slow);
-#if D1_V_NU
+      util = fdiv_nb(a, dreq, rbd, slow);
       int nu = 0;
-      if (cur > ready) nu = fdiv_nb(a, dcur, __builtin_amdgcn_rcpf((float)dcur), slow);
-#else
-      const int nu = fdiv_nb(a, dcur, __builtin_amdgcn_rcpf((float)dcur), slow);
-#endif
+      if (cur > ready) nu = fdiv_nb(a, dcur, rbc, slow);
       if (__builtin_expect(metric && slow, 0))  // exact 64-bit quotient
         util = (int)(((long long)usage * 100) / ((long long)ready * req));
       const bool unready_up = cur > ready && util > target;  // ratio > 1 <=> util > target
@@ -604,17 +554,14 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       int c = q + (exactm ? 0 : 1);
       if (__builtin_expect(metric && !keep && (exactm || slow2), 0))  // binary64 as the spec writes it
         c = (int)ceil(((double)u / (double)target) * (double)base);
-      const int pe = unready_up ? max(cur, c) : c;
-      proposal = (metric && !keep) ? pe : cur;
+      const int pe2 = unready_up ? max(cur, c) : c;
+      proposal = (metric && !keep) ? pe2 : cur;
     }
-    const bool ran = metric;
-    const bool hpa_path = !(cur == 0 && minr != 0);
-    const bool util_valid = metric;
-    D1_STAMP(8);
-    if constexpr (STAMPS) st_acc[11] += __ballot(ran && proposal != cur) != 0 ? 1 : 0;
-    // stabilisation (packed min / max over the records inside each window) and
-    // the rate limits; desired == cur exactly when proposal == cur
-    int desired = cur > mx ? mx : (cur < minr && hpa_path ? minr : cur);
+    o.util = util;
+    o.proposal = proposal;
+    o.ran = metric;
+    o.hpa_path = !(cur == 0 && minr != 0);
+    int desired = cur > mx ? mx : (cur < minr && o.hpa_path ? minr : cur);
     {
       int upr = proposal, dnr = proposal;
       if (rup.stab_mask) {  // wave-uniform
@@ -630,7 +577,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         for (int w = 1; w < 4; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
         dnr = max(dnr, max((int)a.x, (int)a.y));
       }
-      int rc = min(max(cur, upr), dnr);
+      const int rc = min(max(cur, upr), dnr);
       int lo = minr, hi = mx;
       if constexpr (BDEF) {
         // up: max(Percent 100 -> ceil(2.0*cur), Pods 4 -> cur+4) over 15 s
@@ -639,428 +586,453 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         hi = rc > cur ? min(hi, max(2 * cur, cur + 4)) : hi;
         lo = rc < cur ? max(lo, 0) : lo;
       } else {
-        if (ran && proposal != cur) {
+        if (metric && proposal != cur) {
           if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
           else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
         }
       }
       const int db = rc < lo ? lo : (rc > hi ? hi : rc);
-      if (ran && !(ablate & 8)) desired = db;
+      if (metric && !(ablate & 8)) desired = db;
     }
-    D1_STAMP(9);
-    // records clamp to int16 (replicas stay in [0, 32767]; min/max commute with clamping)
-    {
-      const int rv = min(max(proposal, -D1_REC_SAT - 1), D1_REC_SAT);
-      ring_push(hdn, ran ? rv : (int)0x8000);
-      if constexpr (!BDEF) {
-        ring_push(hup, ran ? rv : 0x7FFF);
-        ring_push(hdel, (hpa_path && desired != cur) ? desired - cur : 0);
+    o.desired = desired;
+    return o;
+  };
+  // records clamp to int16 (replicas stay in [0, 32767]; min/max commute with clamping)
+  auto hpa_commit = [&](const HpaOut& h, int cur) {
+    const int rv = min(max(h.proposal, -D1_REC_SAT - 1), D1_REC_SAT);
+    ring_push(hdn, h.ran ? rv : (int)0x8000);
+    if constexpr (!BDEF) {
+      ring_push(hup, h.ran ? rv : 0x7FFF);
+      ring_push(hdel, (h.hpa_path && h.desired != cur) ? h.desired - cur : 0);
+    }
+  };
+  // ---- H. per-node energy (SEMANTICS §3.H, exact integer nanowatt-minutes) ----
+  // use = min(pods * upp, alloc) with sallocr = 0 on nodes not ready; pods <
+  // 2^15 and upp < 2^16 keep every product in 32 bits (all operands uint32:
+  // a mixed int/unsigned min() resolves to the double overload)
+  auto upp_of = [&](int L, float rbp) {
+    const int rcapv = rpods * limit;
+    const int usage = max((limit > 0 && rcapv < L) ? rcapv : L, 0);
+    bool slow = false;
+    int upp = fdiv_nb(usage, max(rpods, 1), rbp, slow);
+    if (__builtin_expect(slow, 0)) upp = usage / max(rpods, 1);
+    return rpods > 0 ? upp : 0;
+  };
+  auto dyn_energy = [&](int upp) -> long long {
+    if (__builtin_expect(upp <= 0xFFFF, 1)) {
+      unsigned long long ed = 0;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        const uint32_t use = min((uint32_t)spods[n] * (uint32_t)upp, (uint32_t)sallocr[n]);  // both uint32: v_min_u32
+        ed += (unsigned long long)sdyn[n] * use;
       }
+      return (long long)ed;
     }
-    replicas = desired;
+    long long e = 0;
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n) {
+      const uint64_t prod = (uint64_t)(uint32_t)spods[n] * (uint64_t)(uint32_t)upp;
+      const uint32_t al = (uint32_t)sallocr[n];
+      const uint32_t use = prod < (uint64_t)al ? (uint32_t)prod : al;
+      e += (long long)((uint64_t)sdyn[n] * use);
+    }
+    return e;
+  };
 
-    D1_STAMP(2);
-    // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
-    if (placed > replicas) {
-      int excess = placed - replicas;
-      placed = replicas;
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
-        if (!m || excess <= 0) continue;  // skipped by the wave when no lane needs the pass
-        int removed = 0, removed_c = 0;
-#pragma unroll
-        for (int n = MAXN - 1; n >= 0; --n) {  // branch-free: k = 0 leaves the slot untouched
-          const int k = (m >> n & 1u) ? min(spods[n], excess) : 0;
-          spods[n] -= k;
-          excess -= k;
-          removed += k;
-          if (pass == 1) removed_c += ((cmask & ~taint()) >> n & 1u) ? k : 0;
-          slc[n] = k > 0 ? t + scas[n] : slc[n];
-        }
-        if (pass == 1) { rpods -= removed; Ffree += removed_c; acc_dirty = acc_dirty || removed > 0; }
-      }
-    }
-    // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
-    int pd = replicas - placed;
-    if (pd > 0) {
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask & ~taint();
-        if (!m || pd <= 0) continue;  // skipped by the wave when no lane needs the pass
-        int added = 0;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) {  // branch-free first fit
-          const int fr = (m >> n & 1u) ? scap[n] - spods[n] : 0;
-          const int k = min(fr, pd);  // fr, pd >= 0
-          spods[n] += k;
-          pd -= k;
-          added += k;
-          slc[n] = k > 0 ? t + scas[n] : slc[n];
-        }
-        placed += added;
-        if (pass == 0) { rpods += added; Ffree -= added; acc_dirty = acc_dirty || added > 0; }
-      }
-    }
-    D1_STAMP(3);
-    // ---- F2. Karpenter provisioning: claims of min(J, pending) pods ----
-    {
-      uint32_t fm = ~used & slot_mask;
-      if (pd > 0 && fm && !(ablate & 2)) {
-        int q = -1, J = 0, zq = 0, cq = 0;
-        uint32_t cm = 0;
-#pragma unroll
-        for (int qq = MAXP - 1; qq >= 0; --qq) {  // first pool in Karpenter order
-          const uint32_t c = pcm[qq] & capsel;
-          if (qq < NP && c && pJ[qq] > 0) { q = qq; J = pJ[qq]; cm = c; zq = pzi[qq]; cq = pcas[qq]; }
-        }
-        if (q >= 0) {
-          const GLOBAL_AS int2* row = table + ((((int64_t)rh * NZI + zq) * 3 + (cm - 1)) * NW + wi) * JT;
-          while (pd > 0 && fm) {
-            const int slot = __ffs((int)fm) - 1;
-            fm &= fm - 1;
-            const int k = min(J, pd);
-            const int2 e = *(const int2*)(row + k);  // never empty: k <= J
-            const int info = e.y, price = e.x;
-            const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
-            const int rs = t + delay;
-            const int4 ac = s_acc[bk];
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              if (n == slot) {
-                sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13);
-                sready[n] = rs;
-                slc[n] = t + casc(cq);
-                scas[n] = casc(cq);
-                spods[n] = k;
-                sprice[n] = price;
-                scap[n] = cap1;
-                sdyn[n] = (uint32_t)ac.z;
-                salloc[n] = ac.w;
-                sallocr[n] = delay == 0 ? ac.w : 0;
-                sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
-              }
-            }
-            const uint32_t bit = 1u << slot;
-            used |= bit;
-            if (capbit1(bc) & capsel) cmask |= bit;
-#pragma unroll
-            for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
-            placed += k;
-            minscap = min(minscap, cap1);
-            Isum += ((long long)ac.y << 32) | (unsigned)ac.x;  // idle draw from launch on
-            if (delay == 0) {
-              rdy |= bit;
-              rpods += k;
-              acc_dirty = true;
-              if (cmask & bit) Ffree += cap1 - k;
-            }
-            else next_ready = min(next_ready, rs);
-            if (bc == 0) nsp++; else nod++;
-            burn += price;
-            launches++;
-            last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
-            hash = (hash ^ last_choice) * 16777619u;
-            step_last_type = bk;
-            flags |= 2u;
-            pd -= k;
-          }
-        }
-      }
-    }
+  // ---- scheduler state ----
+  int t = 0;      // this lane's next step
+  int nxt = 0;    // first step that must take the event path (the first step always does)
+  int tq = 0;     // steps [tq, t) were quiet: their per-step constants are added at the next flush
+  bool stall = false;
+  // per-step constants of the quiet steps since the last event (SEMANTICS §3.H)
+  auto flush = [&](int upto) {
+    const int n = upto - tq;
+    cost += (burn + base_price) * (long long)n;
+    e_hour += (base_nw + Isum) * (long long)n;
+    pend_min += (replicas - rpods) * n;
+    nmin_spot += nsp * n;
+    nmin_od += nod * n;
+    tq = upto;
+  };
 
-    D1_STAMP(4);
-    // ---- G. disruption (SEMANTICS §3.G) ----
-    // Candidates are the consolidatable slots (ready, idle >= consolidateAfter:
-    // t >= slc). A deletion needs an empty candidate, or a candidate of a
-    // WhenEmptyOrUnderutilized pool whose pods fit the other compatible ready
-    // slots (F minus its own free space >= its pods, i.e. F >= its capacity),
-    // which needs F >= the smallest node capacity. That gate costs a few
-    // instructions per slot; the exact sequential evaluation runs only in the
-    // lanes it admits (and only in waves where one does).
-    uint32_t elig = 0, emp = 0;
-#pragma unroll
-    for (int n = MAXN - 1; n >= 0; --n) {  // slot masks built by doubling: 2 VALU per slot and mask
-      elig = 2 * elig + (slc[n] <= t ? 1u : 0u);
-      emp = 2 * emp + (spods[n] == 0 ? 1u : 0u);
+  // load column: the scenario's own trace, or its shared trace (policy sweeps)
+  const int32_t* lp = p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
+  const long long lsl = opq(p.NL);
+  // load-sample ring of this wave
+  const uint32_t ring_off = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(((uint32_t)p.K * 16u + 255u) / 256u * 256u + (threadIdx.x / WAVE) * (uint32_t)D1_RING_BYTES));
+  // LDS byte address (the low word of the generic address of an LDS object)
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)s_acc + ring_off;
+  const int* const ring = reinterpret_cast<const int*>(reinterpret_cast<const char*>(s_acc) + ring_off);
+  int tf = 0;  // trace rows issued (wave-uniform)
+  {
+    const int n0 = min(T, D1_VMN + 2 * D1_K);
+    for (; tf < n0; ++tf) d1_dma_row(lp + (int64_t)tf * lsl, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
+    d1_wait_all();
+  }
+  int t_rdy = tf;  // rows < t_rdy have landed (wave-uniform)
+
+  for (int it = 0;; ++it) {
+    const bool live = t < T;
+    if (__ballot(live) == 0) break;  // wave-uniform
+    d1_wait_rows();
+    t_rdy = max(t_rdy, tf - D1_VMN);
+    bool adv = false;
+    int4 rec = make_int4(0, 0, 0, 0);
+    const int ts = t;
+
+    D1_STAMP(8);
+    // ---- quiet step ----
+    if (live && !stall && t < t_rdy) {
+      const int L = ring[(t & (D1_RB - 1)) * WAVE + lane];
+      stall = t >= nxt;
+      if constexpr (BDEF && D1_LEAN_V) {
+        // Upstream default behavior, decided without the general path:
+        // keep (util inside the tolerance band) leaves the replicas; a
+        // proposal above cur changes nothing at maxReplicas; one below cur
+        // changes nothing while the down window holds a record >= cur
+        // (q_hit) or at minReplicas. util and the proposal ceil(u*ready/target)
+        // are f32-reciprocal divisions with exact remainder corrections on
+        // 24-bit products; anything outside their exact range, the unready
+        // rule, an exact-multiple proposal (binary64 in the spec) or any
+        // replica change is an event.
+        if (!stall) {
+          const int cur = replicas;
+          const int usage = min(L, q_rcap);
+          const int a = (int)__umul24((uint32_t)usage, 100u);
+          int util = (int)((float)a * q_rbd);
+          const int ra = a - (int)__umul24((uint32_t)util, (uint32_t)q_dreq);
+          util += (ra >= q_dreq ? 1 : 0) - (ra < 0 ? 1 : 0);
+          // unready pods and util above target: every replica counted, unready ones idle
+          const bool unr_up = q_unr && util > target;
+          int u = util, base = rpods;
+          if (unr_up) {
+            int nu = (int)((float)a * q_rbc);
+            const int rn = a - (int)__umul24((uint32_t)nu, (uint32_t)q_dcur);
+            nu += (rn >= q_dcur ? 1 : 0) - (rn < 0 ? 1 : 0);
+            u = nu;
+            base = cur;
+          }
+          const bool keep = (uint32_t)(u - ulo) <= (uint32_t)(uhi - ulo) || (unr_up && u < target);
+          const int x = (int)__umul24((uint32_t)u, (uint32_t)base);
+          int c = (int)((float)x * rtarget);
+          int rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
+          c += (rc >= target ? 1 : 0) - (rc < 0 ? 1 : 0);
+          rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
+          const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
+          const bool bad = met && ((uint32_t)usage >= (1u << 20) || (uint32_t)util >= (1u << 16) ||
+                                   (uint32_t)u >= (1u << 16) || (uint32_t)rc >= (uint32_t)target ||
+                                   (unr_up && q_dcur >= (1 << 24)));
+          if (__builtin_expect(met && !bad && !keep && rc == 0, 0))  // binary64 as the spec writes it
+            c = (int)ceil(((double)u / (double)target) * (double)base);
+          else
+            c += rc != 0 ? 1 : 0;
+          const int pr = met && !keep ? (unr_up ? max(cur, c) : c) : cur;
+          const bool hold = pr == cur || (pr > cur ? cur >= mx : (q_hit >= t - wl || cur <= minr));
+          stall = q_mode > 1 || bad || !hold;
+          if (!stall) {
+            ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
+            q_hit = met && pr >= cur ? t : q_hit;
+            int upp = (int)((float)usage * q_rbp);
+            const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
+            upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
+            if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+            else e_hour += dyn_energy(upp);
+            const int pending = cur - rpods;
+            const bool slo_b = pending > 0 || (met && util > slo_util);
+            slo += slo_b ? 1 : 0;
+            const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
+            rec = make_int4(cur, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
+            adv = true;
+          }
+        }
+      } else if (!stall) {
+        const HpaOut h = hpa_eval(L, replicas, rpods, q_rbd, q_rbc);
+        stall = h.desired != replicas;
+        if (!stall) {
+          hpa_commit(h, replicas);
+          const int upp = upp_of(L, q_rbp);
+          if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+          else e_hour += dyn_energy(upp);
+          const int pending = replicas - rpods;
+          const bool slo_b = pending > 0 || (h.ran && h.util > slo_util);
+          slo += slo_b ? 1 : 0;
+          const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
+          rec = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
+          adv = true;
+        }
+      }
     }
-    elig &= rdy;
-    emp &= used;
-    uint32_t weou = 0;
-#pragma unroll
-    for (int q = 0; q < MAXP; ++q)
-      if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) weou |= pmask[q];
-    const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)));
-    if constexpr (STAMPS) st_acc[10] += __ballot(gate != 0) != 0 ? 1 : 0;
-    // DRIFT: ready replacements take over (G1); drifted ready nodes not yet
-    // being replaced are drift candidates (G0)
-    const uint32_t tkm = DRIFT ? (repm & rdy) : 0u;
-    const uint32_t dwork = DRIFT ? (dmask & rdy & ~srcm) : 0u;
-    if ((gate || tkm || dwork) && !(ablate & 1)) {
-      bool any_del = false;
-      // free capacity of the compatible ready untainted slots, from scratch
-      auto ffree_now = [&]() {
-        int f = 0;
-        const uint32_t m = rdy & cmask & ~taint();
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) f += (m >> n & 1u) ? scap[n] - spods[n] : 0;
-        Ffree = f;
-      };
-      auto masks_now = [&]() {
-        uint32_t el = 0, em = 0;
-#pragma unroll
-        for (int n = MAXN - 1; n >= 0; --n) {
-          el = 2 * el + (slc[n] <= t ? 1u : 0u);
-          em = 2 * em + (spods[n] == 0 ? 1u : 0u);
-        }
-        elig = el & rdy;
-        emp = em & used;
-      };
-      // a slot leaves the cluster (its pods are gone or moved already)
-      auto drop_slot = [&](int b) {
-        uint32_t binfo = 0;
-        int bprice = 0;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n)
-          if (n == b) {
-            binfo = sinfo[n];
-            bprice = sprice[n];
-            sallocr[n] = 0;
-            spods[n] = 0;
-            sinfo[n] = 0;
+    D1_STAMP(1);
+    // ---- event steps: every D1_K iterations, or when no lane can step quietly ----
+    const uint64_t sb = __ballot(stall);
+    if constexpr (STAMPS) st_acc[9] += 1;
+    if (sb != 0 && ((it & (D1_K - 1)) == D1_K - 1 || __ballot(adv) == 0 ||
+                    (D1_LAG_V > 0 && __ballot(stall && t + D1_LAG_V < t_rdy) != 0))) {
+      if constexpr (STAMPS) { st_acc[10] += 1; st_acc[11] += __popcll(sb); }
+      // the event step in phases, each a block over the stalled lanes (the
+      // wave-uniform points between them carry the diagnostic stamps)
+      const bool ev = stall;
+      int L = 0, minute = 0, rh = 0, pd = 0, step_last_type = 0xFFFF;
+      uint32_t flags = 0;
+      bool g_acted = false;
+      HpaOut hp{};
+      if (ev) {
+        stall = false;
+        adv = true;
+        L = ring[(t & (D1_RB - 1)) * WAVE + lane];
+        flush(t);
+        minute = (sm0 + t) % 1440;
+        const int h = minute / 60;
+        rh = r * 24 + h;
+        if (h != hour) {  // this hour's prices and carbon intensity
+          if (hour >= 0) {
+            gco2 += (double)e_hour * (ci_min * 1e-9);  // carbon of the hour that ended
+            energy_nw += e_hour;
           }
-        if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
-        burn -= bprice;
-        const int4 ac = s_acc[binfo & 1023u];
-        Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
-        const uint32_t nb = ~(1u << b);
-        used &= nb; rdy &= nb; cmask &= nb; dmask &= nb; srcm &= nb; repm &= nb;
-#pragma unroll
-        for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
-        deletions++;
-        any_del = true;
-        acc_dirty = true;
-      };
-      if constexpr (DRIFT) {
-        if (tkm) {
-          // G1: each ready replacement (slot order) takes its source's pods up
-          // to its free capacity; the rest are evicted; the source is deleted
-          uint32_t tk = tkm;
-          while (tk) {
-            const int m = __ffs((int)tk) - 1;
-            tk &= tk - 1;
-            uint32_t xm = 0;
-            int capm = 0, podm = 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n)
-              if (n == m) { xm = sinfo[n]; sinfo[n] = xm & 0xFFFFu; capm = scap[n]; podm = spods[n]; }
-            const int src = (int)(xm >> 16 & 31u) - 1;
-            int sp = 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) sp = n == src ? spods[n] : sp;
-            const int k = (capbit1((int)(xm >> 12 & 1u)) & capsel) ? min(capm - podm, sp) : 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n)
-              if (n == m) { spods[n] += k; slc[n] = t + scas[n]; }
-            rpods -= sp - k;
-            placed -= sp - k;
-            repm &= ~(1u << m);
-            drop_slot(src);
-            flags |= 4u;
-          }
-          ffree_now();
-          masks_now();
-        }
-      }
-      // PDB evictions allowed (32-bit: pct <= 100 and replicas <= 32767)
-      int allowed = 0x7fffffff;
-      if (pdb_pct >= 0) {
-        const int rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
-        allowed = max(rdyp - (int)(((uint32_t)(pdb_pct * reps) + 99u) / 100u), 0);
-      }
-#pragma unroll
-      for (int q = 0; q < MAXP; ++q) {
-        if (q >= NP) break;
-        const int npool = __popc(pmask[q]);
-        if (npool == 0) continue;
-        const int qbudget = (budget[q] * npool + 99) / 100;
-        const bool weou_q = ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
-        int deleted = 0;
-        if constexpr (DRIFT) {
-          // G0: drifted ready nodes of the pool in slot order, sharing its budget
-          uint32_t dc = dmask & rdy & ~srcm & pmask[q];
-          bool acted = false;
-          while (dc && deleted < qbudget) {
-            const int best = __ffs((int)dc) - 1;
-            dc &= dc - 1;
-            int bp = 0;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) bp = n == best ? spods[n] : bp;
-            const int pdbp = pdb_member ? bp : 0;
-            if (pdbp > allowed) continue;
-            acted = true;
-            // pods move first-fit onto ready, non-drifted, untainted compatible nodes
-            const uint32_t recv = rdy & ~dmask & ~taint() & cmask;
-            int need = bp;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
-              const int k = min(fr, need);
-              spods[n] += k;
-              need -= k;
-              slc[n] = k > 0 ? t + scas[n] : slc[n];
-            }
-            // the rest: a pre-spun replacement under the pool's current
-            // requirements (the F launch rule: the argmin table row), else eviction
-            const uint32_t fr = ~used & slot_mask;
-            int2 e = make_int2(0, -1);
-            uint32_t cmq = 0;
-            int cq = 0;
-            if (need > 0 && fr) {
-              int J = 0, zq = -1;
-#pragma unroll
-              for (int qq = 0; qq < MAXP; ++qq)
-                if (qq == q) { J = pJ[qq]; zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
-              if (cmq && zq >= 0 && need <= J)
-                e = *(const int2*)(table + ((((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * NW + wi) * JT + need);
-            }
-            if (e.y >= 0 && need > 0) {
-              const int info = e.y, price = e.x;
-              const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
-              const int slot = __ffs((int)fr) - 1;
-              const int rs = t + delay;
-              const int4 ac = s_acc[bk];
-#pragma unroll
-              for (int n = 0; n < MAXN; ++n) {
-                if (n == slot) {
-                  sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13 | (best + 1) << 16);
-                  sready[n] = rs;
-                  slc[n] = t + casc(cq);
-                  scas[n] = casc(cq);
-                  spods[n] = 0;
-                  sprice[n] = price;
-                  scap[n] = cap1;
-                  sdyn[n] = (uint32_t)ac.z;
-                  salloc[n] = ac.w;
-                  sallocr[n] = delay == 0 ? ac.w : 0;
-                  sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
-                }
-                if (n == best) spods[n] = need;
-              }
-              const uint32_t bit = 1u << slot;
-              used |= bit;
-              if (capbit1(bc) & capsel) cmask |= bit;
-#pragma unroll
-              for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
-              if (delay == 0) {
-                rdy |= bit;
-                acc_dirty = true;
-              } else {
-                next_ready = min(next_ready, rs);
-              }
-              minscap = min(minscap, cap1);
-              Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
-              if (bc == 0) nsp++; else nod++;
-              burn += price;
-              launches++;
-              last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
-              hash = (hash ^ last_choice) * 16777619u;
-              step_last_type = bk;
-              srcm |= 1u << best;
-              repm |= bit;
-              flags |= 2u | 16u | 32u;
-            } else {
-              rpods -= need;
-              placed -= need;
-              drop_slot(best);
-              flags |= 4u | 16u;
-            }
-            allowed -= pdbp;
-            deleted++;
-          }
-          if (acted) {
-            ffree_now();
-            masks_now();
-          }
-        }
-        while (deleted < qbudget) {
-          const uint32_t cand = elig & pmask[q] & ~taint();
-          const uint32_t ce = cand & emp;
-          if (!ce && !(weou_q && (cand & ~emp) && (Ffree >= minscap || (cand & ~emp & ~cmask)))) break;
-          int best = -1, bpods = 0, bprice = -1, bcap = 0;
-          uint32_t binfo = 0;
-          if (ce) {
-            // empty candidates come first (pods asc): the highest price, then
-            // the lowest slot; deleting one moves nothing
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              const bool c = (ce >> n & 1u) && sprice[n] > bprice;
-              best = c ? n : best;
-              bprice = c ? sprice[n] : bprice;
-              bcap = c ? scap[n] : bcap;
-              binfo = c ? sinfo[n] : binfo;
-            }
-          } else {
-            // under-utilised candidates (pods asc, price desc, slot asc), valid
-            // when their pods fit the other compatible ready slots (F minus
-            // their own free space) and the PDB allows evicting them
-            unsigned long long bkey = ~0ull;
-#pragma unroll
-            for (int n = 0; n < MAXN; ++n) {
-              const int pods = spods[n];
-              const int need = (cmask >> n & 1u) ? scap[n] : pods;
-              const bool ok = (cand >> n & 1u) && need <= Ffree && (!pdb_member || pods <= allowed);
-              const unsigned long long key = (unsigned long long)pods << 36 |
-                                             (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
-              const bool c = ok && key < bkey;
-              bkey = c ? key : bkey;
-              bcap = c ? scap[n] : bcap;
-              binfo = c ? sinfo[n] : binfo;
-            }
-            if (bkey != ~0ull) {
-              best = (int)(bkey & 15u);
-              bpods = (int)(bkey >> 36);
-              bprice = 0x7fffffff - (int)((bkey >> 4) & 0x7fffffffull);
-              // move its pods first-fit onto the other compatible ready nodes
-              int need = bpods;
-              const uint32_t recv = rdy & cmask & ~(1u << best) & ~taint();
-#pragma unroll
-              for (int n = 0; n < MAXN; ++n) {
-                const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
-                const int k = min(fr, need);
-                spods[n] += k;
-                need -= k;
-                slc[n] = k > 0 ? t + scas[n] : slc[n];
-              }
-            }
-          }
-          if (best < 0) break;
-          // delete the node (its pods moved between ready nodes: running counts unchanged)
+          e_hour = 0;
+          hour = h;
+          const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
+          ci_min = ci_gpwmin[rh];
+          base_price = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
+          burn = 0;
+          // every slot's price in flight at once (unused slots read entry 0)
+          int np[MAXN];
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
-            sallocr[n] = n == best ? 0 : sallocr[n];
-            spods[n] = n == best ? 0 : spods[n];
+            const uint32_t x = sinfo[n];
+            np[n] = tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
           }
-          if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
-          burn -= bprice;
-          const int4 ac = s_acc[binfo & 1023u];
-          Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
-          // F loses the node's free space and the moved pods: its whole capacity
-          Ffree -= ((rdy & cmask) >> best & 1u) ? bcap : bpods;
-          const uint32_t nb = ~(1u << best);
-          used &= nb; rdy &= nb; cmask &= nb;
-          if constexpr (DRIFT) dmask &= nb;
 #pragma unroll
-          for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
-          if (pdb_member) allowed -= bpods;
-          deleted++;
-          deletions++;
-          any_del = true;
-          acc_dirty = true;
-          flags |= 4u;
-          elig &= nb;
-          emp &= nb;
-          if (bpods > 0) {  // receivers got pods (and a new consolidatable-from step)
+          for (int n = 0; n < MAXN; ++n) {
+            if (used >> n & 1u) {
+              sprice[n] = np[n];
+              burn += np[n];
+            }
+          }
+          refresh_J(rh);
+        }
+      }
+      D1_STAMP(2);
+      if (ev) {
+        // ---- B. readiness ----
+        if (t >= next_ready) {
+          next_ready = 0x7fffffff;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if ((used & ~rdy) >> n & 1u) {
+              if (sready[n] <= t) {
+                rdy |= 1u << n;
+                rpods += spods[n];
+                sallocr[n] = salloc[n];
+                if ((cmask & ~taint()) >> n & 1u) Ffree += scap[n] - spods[n];
+              }
+              else next_ready = min(next_ready, sready[n]);
+            }
+          }
+        }
+        // ---- A. profile ----
+        const bool in_win = ps_raw <= pe_raw ? (minute >= ps_raw && minute < pe_raw)
+                                             : (minute >= ps_raw || minute < pe_raw);
+        const bool peak = pswitch && in_win;
+        const int prof = peak ? CCKA_PROFILE_PEAK : CCKA_PROFILE_OFFPEAK;
+        if (peak) flags |= 1u;
+        q_peak = peak;
+        if (prof != profile) {
+          profile = prof;
+#pragma unroll
+          for (int q = 0; q < MAXP; ++q) {
+            if (q >= NP) break;
+            const D1Patch& x = p.patch[q][prof + 1];
+            if (x.policy) ppol[q] = x.policy;
+            if (x.cas >= 0) pcas[q] = x.cas;
+            if (x.zi >= 0) pzi[q] = x.zi;
+            if (x.cm) pcm[q] = (uint32_t)x.cm;
+          }
+          // consolidateAfter may have changed: per-slot copies and thresholds
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n)
+            if (used >> n & 1u) {
+              const int c = casc(cas_of(sinfo[n]));
+              slc[n] += c - scas[n];
+              scas[n] = c;
+            }
+          refresh_J(rh);
+          if constexpr (DRIFT) {  // the pools' requirements moved: which nodes left them
+            uint32_t dm = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              const uint32_t x = sinfo[n];
+              uint32_t zm = 0, cm = 0;
+#pragma unroll
+              for (int q = 0; q < MAXP; ++q)
+                if ((int)(x >> 13 & 3u) == q) { zm = pzi[q] >= 0 ? p.zml[pzi[q]] : 0u; cm = pcm[q]; }
+              const bool drifted = !(zm >> (x >> 10 & 3u) & 1u) || !(cm & capbit1((int)(x >> 12 & 1u)));
+              dm |= ((used >> n & 1u) && drifted ? 1u : 0u) << n;
+            }
+            dmask = dm;
+          }
+        }
+
+      }
+      D1_STAMP(3);
+      if (ev) {
+        // ---- C. HPA ----
+        const int cur = replicas;
+        hp = hpa_eval(L, cur, rpods, __builtin_amdgcn_rcpf((float)(rpods * req)),
+                                   __builtin_amdgcn_rcpf((float)(cur * req)));
+        hpa_commit(hp, cur);
+        replicas = hp.desired;
+
+        // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
+        if (placed > replicas) {
+          int excess = placed - replicas;
+          placed = replicas;
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass) {
+            const uint32_t m = pass == 0 ? (used & ~rdy) : rdy;
+            if (!m || excess <= 0) continue;  // skipped by the wave when no lane needs the pass
+            int removed = 0, removed_c = 0;
+#pragma unroll
+            for (int n = MAXN - 1; n >= 0; --n) {  // branch-free: k = 0 leaves the slot untouched
+              const int k = (m >> n & 1u) ? min(spods[n], excess) : 0;
+              spods[n] -= k;
+              excess -= k;
+              removed += k;
+              if (pass == 1) removed_c += ((cmask & ~taint()) >> n & 1u) ? k : 0;
+              slc[n] = k > 0 ? t + scas[n] : slc[n];
+            }
+            if (pass == 1) { rpods -= removed; Ffree += removed_c; }
+          }
+        }
+        // ---- E. kube-scheduler (ready slots) / F1. nomination (in-flight slots) ----
+        pd = replicas - placed;
+        if (pd > 0) {
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass) {
+            const uint32_t m = (pass == 0 ? rdy : (used & ~rdy)) & cmask & ~taint();
+            if (!m || pd <= 0) continue;  // skipped by the wave when no lane needs the pass
+            int added = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {  // branch-free first fit
+              const int fr = (m >> n & 1u) ? scap[n] - spods[n] : 0;
+              const int k = min(fr, pd);  // fr, pd >= 0
+              spods[n] += k;
+              pd -= k;
+              added += k;
+              slc[n] = k > 0 ? t + scas[n] : slc[n];
+            }
+            placed += added;
+            if (pass == 0) { rpods += added; Ffree -= added; }
+          }
+        }
+      }
+      D1_STAMP(4);
+      if (ev) {
+        // ---- F2. Karpenter provisioning: claims of min(J, pending) pods ----
+        {
+          uint32_t fm = ~used & slot_mask;
+          if (pd > 0 && fm && !(ablate & 2)) {
+            int q = -1, J = 0, zq = 0, cq = 0;
+            uint32_t cm = 0;
+#pragma unroll
+            for (int qq = MAXP - 1; qq >= 0; --qq) {  // first pool in Karpenter order
+              const uint32_t c = pcm[qq] & capsel;
+              if (qq < NP && c && pJ[qq] > 0) { q = qq; J = pJ[qq]; cm = c; zq = pzi[qq]; cq = pcas[qq]; }
+            }
+            if (q >= 0) {
+              const GLOBAL_AS int2* row = table + ((((int64_t)rh * NZI + zq) * 3 + (cm - 1)) * NW + wi) * JT;
+              while (pd > 0 && fm) {
+                const int slot = __ffs((int)fm) - 1;
+                fm &= fm - 1;
+                const int k = min(J, pd);
+                const int2 e = *(const int2*)(row + k);  // never empty: k <= J
+                const int info = e.y, price = e.x;
+                const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
+                const int rs = t + delay;
+                const int4 ac = s_acc[bk];
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) {
+                  if (n == slot) {
+                    sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13);
+                    sready[n] = rs;
+                    slc[n] = t + casc(cq);
+                    scas[n] = casc(cq);
+                    spods[n] = k;
+                    sprice[n] = price;
+                    scap[n] = cap1;
+                    sdyn[n] = (uint32_t)ac.z;
+                    salloc[n] = ac.w;
+                    sallocr[n] = delay == 0 ? ac.w : 0;
+                    sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
+                  }
+                }
+                const uint32_t bit = 1u << slot;
+                used |= bit;
+                if (capbit1(bc) & capsel) cmask |= bit;
+#pragma unroll
+                for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
+                placed += k;
+                minscap = min(minscap, cap1);
+                Isum += ((long long)ac.y << 32) | (unsigned)ac.x;  // idle draw from launch on
+                if (delay == 0) {
+                  rdy |= bit;
+                  rpods += k;
+                  if (cmask & bit) Ffree += cap1 - k;
+                }
+                else next_ready = min(next_ready, rs);
+                if (bc == 0) nsp++; else nod++;
+                burn += price;
+                launches++;
+                last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+                hash = (hash ^ last_choice) * 16777619u;
+                step_last_type = bk;
+                flags |= 2u;
+                pd -= k;
+              }
+            }
+          }
+        }
+
+      }
+      D1_STAMP(5);
+      if (ev) {
+        // ---- G. disruption (SEMANTICS §3.G) ----
+        // Candidates are the consolidatable slots (ready, idle >= consolidateAfter:
+        // t >= slc). A deletion needs an empty candidate, or a candidate of a
+        // WhenEmptyOrUnderutilized pool whose pods fit the other compatible ready
+        // slots (F minus its own free space >= its pods, i.e. F >= its capacity),
+        // which needs F >= the smallest node capacity. That gate costs a few
+        // instructions per slot; the exact sequential evaluation runs only in the
+        // lanes it admits (and only in waves where one does).
+        uint32_t elig = 0, emp = 0;
+#pragma unroll
+        for (int n = MAXN - 1; n >= 0; --n) {  // slot masks built by doubling: 2 VALU per slot and mask
+          elig = 2 * elig + (slc[n] <= t ? 1u : 0u);
+          emp = 2 * emp + (spods[n] == 0 ? 1u : 0u);
+        }
+        elig &= rdy;
+        emp &= used;
+        uint32_t weou = 0;
+#pragma unroll
+        for (int q = 0; q < MAXP; ++q)
+          if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) weou |= pmask[q];
+        const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)));
+        // DRIFT: ready replacements take over (G1); drifted ready nodes not yet
+        // being replaced are drift candidates (G0)
+        const uint32_t tkm = DRIFT ? (repm & rdy) : 0u;
+        const uint32_t dwork = DRIFT ? (dmask & rdy & ~srcm) : 0u;
+        if ((gate || tkm || dwork) && !(ablate & 1)) {
+          bool any_del = false;
+          // free capacity of the compatible ready untainted slots, from scratch
+          auto ffree_now = [&]() {
+            int f = 0;
+            const uint32_t m = rdy & cmask & ~taint();
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) f += (m >> n & 1u) ? scap[n] - spods[n] : 0;
+            Ffree = f;
+          };
+          auto masks_now = [&]() {
             uint32_t el = 0, em = 0;
 #pragma unroll
             for (int n = MAXN - 1; n >= 0; --n) {
@@ -1069,91 +1041,378 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             }
             elig = el & rdy;
             emp = em & used;
+          };
+          // a slot leaves the cluster (its pods are gone or moved already)
+          auto drop_slot = [&](int b) {
+            uint32_t binfo = 0;
+            int bprice = 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n)
+              if (n == b) {
+                binfo = sinfo[n];
+                bprice = sprice[n];
+                sallocr[n] = 0;
+                spods[n] = 0;
+                sinfo[n] = 0;
+              }
+            if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
+            burn -= bprice;
+            const int4 ac = s_acc[binfo & 1023u];
+            Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
+            const uint32_t nb = ~(1u << b);
+            used &= nb; rdy &= nb; cmask &= nb; dmask &= nb; srcm &= nb; repm &= nb;
+#pragma unroll
+            for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
+            deletions++;
+            any_del = true;
+          };
+          if constexpr (DRIFT) {
+            if (tkm) {
+              // G1: each ready replacement (slot order) takes its source's pods up
+              // to its free capacity; the rest are evicted; the source is deleted
+              uint32_t tk = tkm;
+              while (tk) {
+                const int m = __ffs((int)tk) - 1;
+                tk &= tk - 1;
+                uint32_t xm = 0;
+                int capm = 0, podm = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n)
+                  if (n == m) { xm = sinfo[n]; sinfo[n] = xm & 0xFFFFu; capm = scap[n]; podm = spods[n]; }
+                const int src = (int)(xm >> 16 & 31u) - 1;
+                int sp = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) sp = n == src ? spods[n] : sp;
+                const int k = (capbit1((int)(xm >> 12 & 1u)) & capsel) ? min(capm - podm, sp) : 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n)
+                  if (n == m) { spods[n] += k; slc[n] = t + scas[n]; }
+                rpods -= sp - k;
+                placed -= sp - k;
+                repm &= ~(1u << m);
+                drop_slot(src);
+                flags |= 4u;
+              }
+              ffree_now();
+              masks_now();
+            }
+          }
+          // PDB evictions allowed (32-bit: pct <= 100 and replicas <= 32767)
+          int allowed = 0x7fffffff;
+          if (pdb_pct >= 0) {
+            const int rdyp = pdb_member ? rpods : 0, reps = pdb_member ? replicas : 0;
+            allowed = max(rdyp - (int)(((uint32_t)(pdb_pct * reps) + 99u) / 100u), 0);
+          }
+#pragma unroll
+          for (int q = 0; q < MAXP; ++q) {
+            if (q >= NP) break;
+            const int npool = __popc(pmask[q]);
+            if (npool == 0) continue;
+            const int qbudget = (budget[q] * npool + 99) / 100;
+            const bool weou_q = ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED;
+            int deleted = 0;
+            if constexpr (DRIFT) {
+              // G0: drifted ready nodes of the pool in slot order, sharing its budget
+              uint32_t dc = dmask & rdy & ~srcm & pmask[q];
+              bool acted = false;
+              while (dc && deleted < qbudget) {
+                const int best = __ffs((int)dc) - 1;
+                dc &= dc - 1;
+                int bp = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) bp = n == best ? spods[n] : bp;
+                const int pdbp = pdb_member ? bp : 0;
+                if (pdbp > allowed) continue;
+                acted = true;
+                // pods move first-fit onto ready, non-drifted, untainted compatible nodes
+                const uint32_t recv = rdy & ~dmask & ~taint() & cmask;
+                int need = bp;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) {
+                  const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
+                  const int k = min(fr, need);
+                  spods[n] += k;
+                  need -= k;
+                  slc[n] = k > 0 ? t + scas[n] : slc[n];
+                }
+                // the rest: a pre-spun replacement under the pool's current
+                // requirements (the F launch rule: the argmin table row), else eviction
+                const uint32_t fr = ~used & slot_mask;
+                int2 e = make_int2(0, -1);
+                uint32_t cmq = 0;
+                int cq = 0;
+                if (need > 0 && fr) {
+                  int J = 0, zq = -1;
+#pragma unroll
+                  for (int qq = 0; qq < MAXP; ++qq)
+                    if (qq == q) { J = pJ[qq]; zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
+                  if (cmq && zq >= 0 && need <= J)
+                    e = *(const int2*)(table + ((((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * NW + wi) * JT + need);
+                }
+                if (e.y >= 0 && need > 0) {
+                  const int info = e.y, price = e.x;
+                  const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
+                  const int slot = __ffs((int)fr) - 1;
+                  const int rs = t + delay;
+                  const int4 ac = s_acc[bk];
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) {
+                    if (n == slot) {
+                      sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13 | (best + 1) << 16);
+                      sready[n] = rs;
+                      slc[n] = t + casc(cq);
+                      scas[n] = casc(cq);
+                      spods[n] = 0;
+                      sprice[n] = price;
+                      scap[n] = cap1;
+                      sdyn[n] = (uint32_t)ac.z;
+                      salloc[n] = ac.w;
+                      sallocr[n] = delay == 0 ? ac.w : 0;
+                      sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
+                    }
+                    if (n == best) spods[n] = need;
+                  }
+                  const uint32_t bit = 1u << slot;
+                  used |= bit;
+                  if (capbit1(bc) & capsel) cmask |= bit;
+#pragma unroll
+                  for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
+                  if (delay == 0) rdy |= bit;
+                  else next_ready = min(next_ready, rs);
+                  minscap = min(minscap, cap1);
+                  Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
+                  if (bc == 0) nsp++; else nod++;
+                  burn += price;
+                  launches++;
+                  last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+                  hash = (hash ^ last_choice) * 16777619u;
+                  step_last_type = bk;
+                  srcm |= 1u << best;
+                  repm |= bit;
+                  flags |= 2u | 16u | 32u;
+                } else {
+                  rpods -= need;
+                  placed -= need;
+                  drop_slot(best);
+                  flags |= 4u | 16u;
+                }
+                allowed -= pdbp;
+                deleted++;
+              }
+              if (acted) {
+                g_acted = true;
+                ffree_now();
+                masks_now();
+              }
+            }
+            while (deleted < qbudget) {
+              const uint32_t cand = elig & pmask[q] & ~taint();
+              const uint32_t ce = cand & emp;
+              if (!ce && !(weou_q && (cand & ~emp) && (Ffree >= minscap || (cand & ~emp & ~cmask)))) break;
+              int best = -1, bpods = 0, bprice = -1, bcap = 0;
+              uint32_t binfo = 0;
+              if (ce) {
+                // empty candidates come first (pods asc): the highest price, then
+                // the lowest slot; deleting one moves nothing
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) {
+                  const bool c = (ce >> n & 1u) && sprice[n] > bprice;
+                  best = c ? n : best;
+                  bprice = c ? sprice[n] : bprice;
+                  bcap = c ? scap[n] : bcap;
+                  binfo = c ? sinfo[n] : binfo;
+                }
+              } else {
+                // under-utilised candidates (pods asc, price desc, slot asc), valid
+                // when their pods fit the other compatible ready slots (F minus
+                // their own free space) and the PDB allows evicting them
+                unsigned long long bkey = ~0ull;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n) {
+                  const int pods = spods[n];
+                  const int need = (cmask >> n & 1u) ? scap[n] : pods;
+                  const bool ok = (cand >> n & 1u) && need <= Ffree && (!pdb_member || pods <= allowed);
+                  const unsigned long long key = (unsigned long long)pods << 36 |
+                                                 (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
+                  const bool c = ok && key < bkey;
+                  bkey = c ? key : bkey;
+                  bcap = c ? scap[n] : bcap;
+                  binfo = c ? sinfo[n] : binfo;
+                }
+                if (bkey != ~0ull) {
+                  best = (int)(bkey & 15u);
+                  bpods = (int)(bkey >> 36);
+                  bprice = 0x7fffffff - (int)((bkey >> 4) & 0x7fffffffull);
+                  // move its pods first-fit onto the other compatible ready nodes
+                  int need = bpods;
+                  const uint32_t recv = rdy & cmask & ~(1u << best) & ~taint();
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) {
+                    const int fr = (recv >> n & 1u) ? scap[n] - spods[n] : 0;
+                    const int k = min(fr, need);
+                    spods[n] += k;
+                    need -= k;
+                    slc[n] = k > 0 ? t + scas[n] : slc[n];
+                  }
+                }
+              }
+              if (best < 0) break;
+              // delete the node (its pods moved between ready nodes: running counts unchanged)
+#pragma unroll
+              for (int n = 0; n < MAXN; ++n) {
+                sallocr[n] = n == best ? 0 : sallocr[n];
+                spods[n] = n == best ? 0 : spods[n];
+              }
+              if ((binfo >> 12 & 1u) == 0) nsp--; else nod--;
+              burn -= bprice;
+              const int4 ac = s_acc[binfo & 1023u];
+              Isum -= ((long long)ac.y << 32) | (unsigned)ac.x;
+              // F loses the node's free space and the moved pods: its whole capacity
+              Ffree -= ((rdy & cmask) >> best & 1u) ? bcap : bpods;
+              const uint32_t nb = ~(1u << best);
+              used &= nb; rdy &= nb; cmask &= nb;
+              if constexpr (DRIFT) dmask &= nb;
+#pragma unroll
+              for (int qq = 0; qq < MAXP; ++qq) pmask[qq] &= nb;
+              if (pdb_member) allowed -= bpods;
+              deleted++;
+              deletions++;
+              any_del = true;
+              flags |= 4u;
+              elig &= nb;
+              emp &= nb;
+              if (bpods > 0) {  // receivers got pods (and a new consolidatable-from step)
+                uint32_t el = 0, em = 0;
+#pragma unroll
+                for (int n = MAXN - 1; n >= 0; --n) {
+                  el = 2 * el + (slc[n] <= t ? 1u : 0u);
+                  em = 2 * em + (spods[n] == 0 ? 1u : 0u);
+                }
+                elig = el & rdy;
+                emp = em & used;
+              }
+            }
+          }
+          if (any_del) {  // capacity of the remaining nodes
+            g_acted = true;
+            minscap = 0x7fffffff;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) minscap = (used >> n & 1u) ? min(minscap, scap[n]) : minscap;
           }
         }
-      }
-      if (any_del) {  // capacity of the remaining nodes
-        minscap = 0x7fffffff;
-#pragma unroll
-        for (int n = 0; n < MAXN; ++n) minscap = (used >> n & 1u) ? min(minscap, scap[n]) : minscap;
-      }
-    }
 
-    D1_STAMP(5);
-    // ---- H. accounting (SEMANTICS §3.H, exact integer nanowatt-minutes) ----
-    // per node use = min(pods * upp, alloc) with sallocr = 0 on nodes not
-    // ready; pods < 2^15 and upp < 2^16 keep every product in 32 bits (all
-    // operands uint32: a mixed int/unsigned min() resolves to the double overload)
-    int upp = 0;
-    {
-      const int rcapv = rpods * limit;
-      const int usage = max((limit > 0 && rcapv < L) ? rcapv : L, 0);
-      bool slow = false;
-      upp = fdiv_nb(usage, max(rpods, 1), __builtin_amdgcn_rcpf((float)rpods), slow);
-      if (__builtin_expect(slow, 0)) upp = usage / max(rpods, 1);
-      upp = rpods > 0 ? upp : 0;
-    }
-#if D1_V_ACC == 1
-    if (acc_dirty) {  // ready pods changed: refresh the cached sums
-      acc_dirty = false;
-      unsigned long long sv = 0;
-      float rv = 0.f;
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] : 0u;
-        sv += (unsigned long long)sdyn[n] * pr;
-        rv = fmaxf(rv, (float)pr * sinv[n]);
       }
-      Ssum = sv;
-      Rmax = rv;
-    }
-    const bool fast_e = (float)upp * Rmax < 0.9999f;  // no node saturates
-#else
-    const bool fast_e = false;
-    (void)Rmax; (void)sinv; (void)acc_dirty;
-#endif
-    long long e_step = base_nw + Isum;
-    if (fast_e) {
-      e_step += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-    } else if (__builtin_expect(upp <= 0xFFFF, 1)) {
-      unsigned long long ed = 0;
+      D1_STAMP(6);
+      if (ev) {
+        // ---- H. accounting (energy from the cached sums unless a node saturates) ----
+        {
+          unsigned long long sv = 0;
+          float rv = 0.f;
 #pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        const uint32_t use = min((uint32_t)spods[n] * (uint32_t)upp, (uint32_t)sallocr[n]);  // both uint32: v_min_u32
-        ed += (unsigned long long)sdyn[n] * use;
+          for (int n = 0; n < MAXN; ++n) {
+            const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] : 0u;
+            sv += (unsigned long long)sdyn[n] * pr;
+            rv = fmaxf(rv, (float)pr * sinv[n]);
+          }
+          Ssum = sv;
+          Rmax = rv;
+        }
+        q_rbp = __builtin_amdgcn_rcpf((float)rpods);
+        const int upp = upp_of(L, q_rbp);
+        long long e_step = base_nw + Isum;
+        if ((float)upp * Rmax < 0.9999f) e_step += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+        else e_step += dyn_energy(upp);
+        cost += burn + base_price;
+        e_hour += e_step;
+        const int pending = replicas - rpods;
+        if (pending > 0 || (hp.ran && hp.util > slo_util)) { slo++; flags |= 8u; }
+        pend_min += pending;
+        nmin_spot += nsp;
+        nmin_od += nod;
+        peak_nodes = max(peak_nodes, nsp + nod);
+        tq = t + 1;
+        rec = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16,
+                        (step_last_type & 0xFFFF) | (int)(flags << 16));
+
+        // ---- caches of the quiet steps that follow ----
+        {
+          q_rbd = __builtin_amdgcn_rcpf((float)(rpods * req));
+          q_rbc = __builtin_amdgcn_rcpf((float)(replicas * req));
+          q_rcap = limit > 0 ? rpods * limit : 0x7fffffff;
+          q_dreq = rpods * req;
+          q_dcur = replicas * req;
+          {
+            const bool met = replicas <= mx && replicas >= minr && rpods > 0 && !(replicas == 0 && minr != 0);
+            const bool hpa_path = !(replicas == 0 && minr != 0);
+            const int dnm = replicas > mx ? mx : (replicas < minr && hpa_path ? minr : replicas);
+            q_mode = met ? (q_dreq < (1 << 24) ? 0 : 2) : (dnm == replicas ? 1 : 2);
+          }
+          q_unr = replicas > rpods;
+          if constexpr (BDEF) {  // newest history record >= the new replica count
+            int hit = -0x40000000;
+#pragma unroll
+            for (int k = CCKA_HIST - 1; k >= 0; --k) {
+              const int e = (int)(short)(hdn[k >> 1] >> (16 * (k & 1)));
+              hit = e >= replicas ? t - k : hit;
+            }
+            q_hit = hit;
+          }
+        }
+        // first step that needs the event path again: a node becomes ready,
+        // an hour or peak-window boundary, a slot becomes a consolidation
+        // candidate that the gate admits (state is unchanged until then, and a
+        // disruption evaluation that acted on nothing acts on nothing again
+        // with the same candidates), or the next step when disruption acted
+        // (the budget may allow more)
+        {
+          int nx = min(next_ready, t + 60 - minute % 60);
+          if (pswitch) {
+            const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;
+            nx = min(nx, t + min(dps, dpe));
+          }
+          uint32_t em = 0;
+#pragma unroll
+          for (int n = MAXN - 1; n >= 0; --n) em = 2 * em + (spods[n] == 0 ? 1u : 0u);
+          em &= used;
+          uint32_t wq = 0;
+#pragma unroll
+          for (int q = 0; q < MAXP; ++q)
+            if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) wq |= pmask[q];
+          const uint32_t gm = rdy & (em | (Ffree >= minscap ? wq : (wq & ~cmask)));
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) nx = ((gm >> n & 1u) && slc[n] > t) ? min(nx, slc[n]) : nx;
+          if (g_acted || (ablate & 15)) nx = t + 1;  // ablation runs: every step an event
+          nxt = nx;
+        }
       }
-      e_step += (long long)ed;
-    } else {
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        const uint64_t prod = (uint64_t)(uint32_t)spods[n] * (uint64_t)(uint32_t)upp;
-        const uint32_t al = (uint32_t)sallocr[n];
-        const uint32_t use = prod < (uint64_t)al ? (uint32_t)prod : al;
-        e_step += (long long)((uint64_t)sdyn[n] * use);
+      D1_STAMP(7);
+    }
+    if (adv) {
+      if (traj) *(int4*)(traj + (int64_t)ts * ls + i) = rec;
+      t = ts + 1;
+    }
+    // ---- ring refill: D1_K rows once every lane has consumed what they overwrite ----
+    if ((it & (D1_K - 1)) == D1_K - 1 && tf < T) {
+      if (__ballot(t < T && t < tf + D1_K - D1_RB) == 0) {
+        const int n1 = min(T, tf + D1_K);
+        for (; tf < n1; ++tf)
+          d1_dma_row(lp + (int64_t)tf * lsl, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
+        if (tf == T) {  // no younger DMA will retire the last rows
+          d1_wait_all();
+          t_rdy = T;
+        }
       }
     }
-    cost += burn + base_price;
-    energy_nw += e_step;
-    e_hour += e_step;
-    const int pending = replicas - rpods;
-    if (pending > 0 || (util_valid && util > slo_util)) { slo++; flags |= 8u; }
-    pend_min += pending;
-    nmin_spot += nsp;
-    nmin_od += nod;
-    peak_nodes = max(peak_nodes, nsp + nod);
-    D1_STAMP(6);
-    rec_prev = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16,
-                         (step_last_type & 0xFFFF) | (int)(flags << 16));
-#pragma unroll
-    for (int k = 0; k + 1 < D1_PF; ++k) Lq[k] = Lq[k + 1];
-    Lq[D1_PF - 1] = opqv(Lraw);
+    D1_STAMP(8);
   }
-  if (traj) *(int4*)(traj + (int64_t)(T - 1) * ls + i) = rec_prev;
-  D1_STAMP(7);
+  d1_wait_all();  // no LDS-DMA may outlive the wave
   if constexpr (STAMPS) {
     if (lane == (__ffsll((long long)__ballot(1)) - 1))
-      for (int k = 0; k < 12; ++k) atomicAdd(&p.stamps[k], (unsigned long long)st_acc[k]);
+      for (int k = 1; k < 12; ++k) atomicAdd(&p.stamps[k], (unsigned long long)st_acc[k]);
+      atomicMax(&p.stamps[0], (unsigned long long)st_acc[9]);  // longest wave (iterations)
   }
+  flush(T);
+  energy_nw += e_hour;
   gco2 += (double)e_hour * (ci_min * 1e-9);
   p.cost[i] = cost;
   p.energy[i] = (double)energy_nw * 1e-9;
@@ -1182,7 +1441,7 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const int B = 256;
   const int64_t waves = (p.N + p.lpw - 1) / p.lpw;
   const unsigned grid = (unsigned)((waves + B / WAVE - 1) / (B / WAVE));
-  const size_t lds = (size_t)p.K * sizeof(int4);
+  const size_t lds = ((size_t)p.K * sizeof(int4) + 255) / 256 * 256 + (size_t)(B / WAVE) * D1_RING_BYTES;
   // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
   if (p.drift) {  // drift (SEMANTICS 3.G0): 8 slots, <= 2 pools (d1_disrupt_ok)
