@@ -312,10 +312,10 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_RB_V 64
 #endif
 #ifndef D1_K_V
-#define D1_K_V 8
+#define D1_K_V 4
 #endif
 #ifndef D1_VMN_V
-#define D1_VMN_V 24
+#define D1_VMN_V 12
 #endif
 #ifndef D1_LEAN_V
 #define D1_LEAN_V 1
@@ -323,11 +323,34 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #ifndef D1_LAG_V
 #define D1_LAG_V 0
 #endif
+#ifndef D1_S_V
+#define D1_S_V 3
+#endif
 constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
 constexpr int D1_K = D1_K_V;      // event cadence and DMA batch (iterations, power of two)
 constexpr int D1_VMN = D1_VMN_V;  // rows in flight (vmcnt bound; <= 63)
-static_assert(D1_VMN + 2 * D1_K < D1_RB, "ring too small for the DMA lead");
+constexpr int D1_S = D1_S_V;      // quiet steps per iteration and lane
+static_assert(D1_VMN + 8 * D1_S <= D1_RB, "ring too small for the DMA lead");
 constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
+
+// streaming hint on the trace rows and trajectory records (build variants)
+#ifndef D1_NT_V
+#define D1_NT_V 0
+#endif
+#if D1_NT_V
+#define D1_NT " nt"
+#else
+#define D1_NT ""
+#endif
+__device__ __forceinline__ void d1_store_rec(GLOBAL_AS int4* p, const int4& v) {
+#if D1_NT_V
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, (GLOBAL_AS i32x4*)p);
+#else
+  *(int4*)p = v;
+#endif
+}
 
 __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row) {
   unsigned keep;
@@ -335,7 +358,7 @@ __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row)
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\t"
+      "global_load_lds_dword %1, off" D1_NT "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(src), "s"(lds_row)
@@ -666,120 +689,42 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int* const ring = reinterpret_cast<const int*>(reinterpret_cast<const char*>(s_acc) + ring_off);
   int tf = 0;  // trace rows issued (wave-uniform)
   {
-    const int n0 = min(T, D1_VMN + 2 * D1_K);
+    const int n0 = min(T, D1_VMN + 4 * D1_S);
     for (; tf < n0; ++tf) d1_dma_row(lp + (int64_t)tf * lsl, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
     d1_wait_all();
   }
   int t_rdy = tf;  // rows < t_rdy have landed (wave-uniform)
+  bool pf_ok = false;
+  bool qadv = true;  // some lane stepped quietly in the last iteration (wave-uniform)
+  int Lpf[D1_S];
+#pragma unroll
+  for (int q = 0; q < D1_S; ++q) Lpf[q] = 0;
+  GLOBAL_AS int4* tp = traj + i;  // this lane's record of step t
 
   for (int it = 0;; ++it) {
     const bool live = t < T;
     if (__ballot(live) == 0) break;  // wave-uniform
     d1_wait_rows();
     t_rdy = max(t_rdy, tf - D1_VMN);
-    bool adv = false;
-    int4 rec = make_int4(0, 0, 0, 0);
-    const int ts = t;
-
-    D1_STAMP(8);
-    // ---- quiet step ----
-    if (live && !stall && t < t_rdy) {
-      const int L = ring[(t & (D1_RB - 1)) * WAVE + lane];
-      stall = t >= nxt;
-      if constexpr (BDEF && D1_LEAN_V) {
-        // Upstream default behavior, decided without the general path:
-        // keep (util inside the tolerance band) leaves the replicas; a
-        // proposal above cur changes nothing at maxReplicas; one below cur
-        // changes nothing while the down window holds a record >= cur
-        // (q_hit) or at minReplicas. util and the proposal ceil(u*ready/target)
-        // are f32-reciprocal divisions with exact remainder corrections on
-        // 24-bit products; anything outside their exact range, the unready
-        // rule, an exact-multiple proposal (binary64 in the spec) or any
-        // replica change is an event.
-        if (!stall) {
-          const int cur = replicas;
-          const int usage = min(L, q_rcap);
-          const int a = (int)__umul24((uint32_t)usage, 100u);
-          int util = (int)((float)a * q_rbd);
-          const int ra = a - (int)__umul24((uint32_t)util, (uint32_t)q_dreq);
-          util += (ra >= q_dreq ? 1 : 0) - (ra < 0 ? 1 : 0);
-          // unready pods and util above target: every replica counted, unready ones idle
-          const bool unr_up = q_unr && util > target;
-          int u = util, base = rpods;
-          if (unr_up) {
-            int nu = (int)((float)a * q_rbc);
-            const int rn = a - (int)__umul24((uint32_t)nu, (uint32_t)q_dcur);
-            nu += (rn >= q_dcur ? 1 : 0) - (rn < 0 ? 1 : 0);
-            u = nu;
-            base = cur;
-          }
-          const bool keep = (uint32_t)(u - ulo) <= (uint32_t)(uhi - ulo) || (unr_up && u < target);
-          const int x = (int)__umul24((uint32_t)u, (uint32_t)base);
-          int c = (int)((float)x * rtarget);
-          int rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
-          c += (rc >= target ? 1 : 0) - (rc < 0 ? 1 : 0);
-          rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
-          const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
-          const bool bad = met && ((uint32_t)usage >= (1u << 20) || (uint32_t)util >= (1u << 16) ||
-                                   (uint32_t)u >= (1u << 16) || (uint32_t)rc >= (uint32_t)target ||
-                                   (unr_up && q_dcur >= (1 << 24)));
-          if (__builtin_expect(met && !bad && !keep && rc == 0, 0))  // binary64 as the spec writes it
-            c = (int)ceil(((double)u / (double)target) * (double)base);
-          else
-            c += rc != 0 ? 1 : 0;
-          const int pr = met && !keep ? (unr_up ? max(cur, c) : c) : cur;
-          const bool hold = pr == cur || (pr > cur ? cur >= mx : (q_hit >= t - wl || cur <= minr));
-          stall = q_mode > 1 || bad || !hold;
-          if (!stall) {
-            ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
-            q_hit = met && pr >= cur ? t : q_hit;
-            int upp = (int)((float)usage * q_rbp);
-            const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
-            upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
-            if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-            else e_hour += dyn_energy(upp);
-            const int pending = cur - rpods;
-            const bool slo_b = pending > 0 || (met && util > slo_util);
-            slo += slo_b ? 1 : 0;
-            const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
-            rec = make_int4(cur, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
-            adv = true;
-          }
-        }
-      } else if (!stall) {
-        const HpaOut h = hpa_eval(L, replicas, rpods, q_rbd, q_rbc);
-        stall = h.desired != replicas;
-        if (!stall) {
-          hpa_commit(h, replicas);
-          const int upp = upp_of(L, q_rbp);
-          if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-          else e_hour += dyn_energy(upp);
-          const int pending = replicas - rpods;
-          const bool slo_b = pending > 0 || (h.ran && h.util > slo_util);
-          slo += slo_b ? 1 : 0;
-          const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
-          rec = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
-          adv = true;
-        }
-      }
-    }
-    D1_STAMP(1);
-    // ---- event steps: every D1_K iterations, or when no lane can step quietly ----
+    // ---- event steps of the stalled lanes: every D1_K iterations, or when no
+    // lane stepped quietly in the last one. They run before this iteration's
+    // quiet steps, so their loads do not wait for this iteration's records
+    // (every load waits for all older memory operations), and a lane leaves
+    // its event step straight into quiet steps ----
     const uint64_t sb = __ballot(stall);
     if constexpr (STAMPS) st_acc[9] += 1;
-    if (sb != 0 && ((it & (D1_K - 1)) == D1_K - 1 || __ballot(adv) == 0 ||
-                    (D1_LAG_V > 0 && __ballot(stall && t + D1_LAG_V < t_rdy) != 0))) {
+    if (sb != 0 && ((it & (D1_K - 1)) == D1_K - 1 || !qadv)) {
       if constexpr (STAMPS) { st_acc[10] += 1; st_acc[11] += __popcll(sb); }
       // the event step in phases, each a block over the stalled lanes (the
       // wave-uniform points between them carry the diagnostic stamps)
       const bool ev = stall;
       int L = 0, minute = 0, rh = 0, pd = 0, step_last_type = 0xFFFF;
+      int4 rec;
       uint32_t flags = 0;
-      bool g_acted = false;
+      bool g_acted = false, hchg = false, jchg = false;
       HpaOut hp{};
       if (ev) {
         stall = false;
-        adv = true;
         L = ring[(t & (D1_RB - 1)) * WAVE + lane];
         flush(t);
         minute = (sm0 + t) % 1440;
@@ -792,25 +737,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           }
           e_hour = 0;
           hour = h;
-          const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
-          ci_min = ci_gpwmin[rh];
-          base_price = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
-          burn = 0;
-          // every slot's price in flight at once (unused slots read entry 0)
-          int np[MAXN];
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            const uint32_t x = sinfo[n];
-            np[n] = tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
-          }
-#pragma unroll
-          for (int n = 0; n < MAXN; ++n) {
-            if (used >> n & 1u) {
-              sprice[n] = np[n];
-              burn += np[n];
-            }
-          }
-          refresh_J(rh);
+          hchg = true;  // prices, carbon intensity and J are loaded before provisioning
         }
       }
       D1_STAMP(2);
@@ -857,7 +784,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               slc[n] += c - scas[n];
               scas[n] = c;
             }
-          refresh_J(rh);
+          jchg = true;
           if constexpr (DRIFT) {  // the pools' requirements moved: which nodes left them
             uint32_t dm = 0;
 #pragma unroll
@@ -929,6 +856,30 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       }
       D1_STAMP(4);
       if (ev) {
+        // ---- the hour's prices and carbon intensity, the pools' J: loaded only
+        // here, after the phases that do not read them, since every load
+        // waits for all older memory operations (this iteration's records) ----
+        if (hchg) {
+          const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
+          ci_min = ci_gpwmin[rh];
+          base_price = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
+          burn = 0;
+          // every slot's price in flight at once (unused slots read entry 0)
+          int np[MAXN];
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            const uint32_t x = sinfo[n];
+            np[n] = tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
+          }
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (used >> n & 1u) {
+              sprice[n] = np[n];
+              burn += np[n];
+            }
+          }
+        }
+        if (hchg || jchg) refresh_J(rh);
         // ---- F2. Karpenter provisioning: claims of min(J, pending) pods ----
         {
           uint32_t fm = ~used & slot_mask;
@@ -1365,7 +1316,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // with the same candidates), or the next step when disruption acted
         // (the budget may allow more)
         {
+#ifdef D1_NOHOUR_TEST
+          int nx = next_ready;  // timing experiment only (wrong results)
+#else
           int nx = min(next_ready, t + 60 - minute % 60);
+#endif
           if (pswitch) {
             const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;
             nx = min(nx, t + min(dps, dpe));
@@ -1385,16 +1340,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           nxt = nx;
         }
       }
+      if (ev) {
+        if (traj) d1_store_rec(tp, rec);
+        tp += ls;
+        ++t;
+      }
+      pf_ok = pf_ok && !ev;
       D1_STAMP(7);
     }
-    if (adv) {
-      if (traj) *(int4*)(traj + (int64_t)ts * ls + i) = rec;
-      t = ts + 1;
-    }
-    // ---- ring refill: D1_K rows once every lane has consumed what they overwrite ----
-    if ((it & (D1_K - 1)) == D1_K - 1 && tf < T) {
-      if (__ballot(t < T && t < tf + D1_K - D1_RB) == 0) {
-        const int n1 = min(T, tf + D1_K);
+    // ---- ring refill: D1_S rows per iteration once every lane has consumed
+    // what they overwrite; issued after the event steps, whose own loads
+    // wait for every older vector-memory operation ----
+    if (tf < T) {
+      if (__ballot(t < T && t < tf + D1_S - D1_RB) == 0) {
+        const int n1 = min(T, tf + D1_S);
         for (; tf < n1; ++tf)
           d1_dma_row(lp + (int64_t)tf * lsl, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
         if (tf == T) {  // no younger DMA will retire the last rows
@@ -1403,13 +1362,120 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         }
       }
     }
+    bool adv = false;
+    if (!pf_ok) {  // a row landed after the prefetch (or the lane left an event step)
+#pragma unroll
+      for (int q = 0; q < D1_S; ++q) Lpf[q] = ring[((t + q) & (D1_RB - 1)) * WAVE + lane];
+    }
+
+    D1_STAMP(8);
+    // ---- quiet steps: up to D1_S per iteration and lane ----
+#pragma unroll
+    for (int sub = 0; sub < D1_S; ++sub) {
+    if (t < T && !stall && t < t_rdy) {
+      // a lane still stepping in sub-step `sub` has advanced in every earlier one
+      const int L = Lpf[sub];
+      int4 rec;
+      stall = t >= nxt;
+      if constexpr (BDEF && D1_LEAN_V) {
+        // Upstream default behavior, decided without the general path:
+        // keep (util inside the tolerance band) leaves the replicas; a
+        // proposal above cur changes nothing at maxReplicas; one below cur
+        // changes nothing while the down window holds a record >= cur
+        // (q_hit) or at minReplicas. util and the proposal ceil(u*ready/target)
+        // are f32-reciprocal divisions with exact remainder corrections on
+        // 24-bit products; anything outside their exact range, the unready
+        // rule, an exact-multiple proposal (binary64 in the spec) or any
+        // replica change is an event.
+        if (!stall) {
+          const int cur = replicas;
+          const int usage = min(L, q_rcap);
+          const int a = (int)__umul24((uint32_t)usage, 100u);
+          int util = (int)((float)a * q_rbd);
+          const int ra = a - (int)__umul24((uint32_t)util, (uint32_t)q_dreq);
+          util += (ra >= q_dreq ? 1 : 0) - (ra < 0 ? 1 : 0);
+          // unready pods and util above target: every replica counted, unready ones idle
+          const bool unr_up = q_unr && util > target;
+          int u = util, base = rpods;
+          if (unr_up) {
+            int nu = (int)((float)a * q_rbc);
+            const int rn = a - (int)__umul24((uint32_t)nu, (uint32_t)q_dcur);
+            nu += (rn >= q_dcur ? 1 : 0) - (rn < 0 ? 1 : 0);
+            u = nu;
+            base = cur;
+          }
+          const bool keep = (uint32_t)(u - ulo) <= (uint32_t)(uhi - ulo) || (unr_up && u < target);
+          const int x = (int)__umul24((uint32_t)u, (uint32_t)base);
+          int c = (int)((float)x * rtarget);
+          int rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
+          c += (rc >= target ? 1 : 0) - (rc < 0 ? 1 : 0);
+          rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
+          const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
+          const bool bad = met && ((uint32_t)usage >= (1u << 20) || (uint32_t)util >= (1u << 16) ||
+                                   (uint32_t)u >= (1u << 16) || (uint32_t)rc >= (uint32_t)target ||
+                                   (unr_up && q_dcur >= (1 << 24)));
+          if (__builtin_expect(met && !bad && !keep && rc == 0, 0))  // binary64 as the spec writes it
+            c = (int)ceil(((double)u / (double)target) * (double)base);
+          else
+            c += rc != 0 ? 1 : 0;
+          const int pr = met && !keep ? (unr_up ? max(cur, c) : c) : cur;
+          const bool hold = pr == cur || (pr > cur ? cur >= mx : (q_hit >= t - wl || cur <= minr));
+          stall = q_mode > 1 || bad || !hold;
+          if (!stall) {
+            ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
+            q_hit = met && pr >= cur ? t : q_hit;
+            int upp = (int)((float)usage * q_rbp);
+            const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
+            upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
+            if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+            else e_hour += dyn_energy(upp);
+            const int pending = cur - rpods;
+            const bool slo_b = pending > 0 || (met && util > slo_util);
+            slo += slo_b ? 1 : 0;
+            const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
+            rec = make_int4(cur, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
+            adv = true;
+            if (traj) d1_store_rec(tp, rec);
+            tp += ls;
+            ++t;
+          }
+        }
+      } else if (!stall) {
+        const HpaOut h = hpa_eval(L, replicas, rpods, q_rbd, q_rbc);
+        stall = h.desired != replicas;
+        if (!stall) {
+          hpa_commit(h, replicas);
+          const int upp = upp_of(L, q_rbp);
+          if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+          else e_hour += dyn_energy(upp);
+          const int pending = replicas - rpods;
+          const bool slo_b = pending > 0 || (h.ran && h.util > slo_util);
+          slo += slo_b ? 1 : 0;
+          const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
+          rec = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
+          adv = true;
+          if (traj) d1_store_rec(tp, rec);
+          tp += ls;
+          ++t;
+        }
+      }
+    }
+    }
+    qadv = __ballot(adv) != 0;
+    D1_STAMP(1);
+    // this lane's next samples (the LDS latency hides under the loop tail);
+    // rows that have not landed yet are read again at the top
+    pf_ok = t + (D1_S - 1) < t_rdy;
+#pragma unroll
+    for (int q = 0; q < D1_S; ++q) Lpf[q] = ring[((t + q) & (D1_RB - 1)) * WAVE + lane];
     D1_STAMP(8);
   }
   d1_wait_all();  // no LDS-DMA may outlive the wave
   if constexpr (STAMPS) {
-    if (lane == (__ffsll((long long)__ballot(1)) - 1))
+    if (lane == (__ffsll((long long)__ballot(1)) - 1)) {
       for (int k = 1; k < 12; ++k) atomicAdd(&p.stamps[k], (unsigned long long)st_acc[k]);
       atomicMax(&p.stamps[0], (unsigned long long)st_acc[9]);  // longest wave (iterations)
+    }
   }
   flush(T);
   energy_nw += e_hour;

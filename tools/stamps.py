@@ -20,9 +20,9 @@ eng.lib.ccka_debug_ablate.argtypes = [C.c_void_p, C.c_int32]
 eng.set_world(configs.config2_world())
 eng.set_scenarios(configs.hpa_scenarios(100_000))
 eng.gen_load(configs.trace_gen())
-names = ["-", "quiet step", "event: flush+hour", "event: readiness+profile",
+names = ["-", "quiet steps", "top (row wait, refill) + event flush+hour", "event: readiness+profile",
          "event: hpa+reconcile+sched", "event: provision", "event: disruption", "event: accounting+nxt",
-         "store+refill+row wait"]
+         "sample prefetch + loop"]
 eng.lib.ccka_debug_ablate(eng.ctx, 16)
 trajectory = "--summary" not in sys.argv
 eng.rollout(trajectory=trajectory)
