@@ -521,7 +521,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int q_rcap = 0, q_dreq = 1, q_dcur = 1;  // usage cap (ready*limit, or INT_MAX without a limit), ready*req, cur*req
   int q_mode = 2;               // 0: metric (ready*req < 2^24), 1: no metric and replicas in range, 2: events only
   bool q_unr = false;           // unready pods
-  int q_hit = -0x40000000;      // last step whose recorded proposal >= cur (down window hold)
+  int q_hold = -0x40000000;     // the down window holds a record >= cur up to this step
+  bool q_atmax = false, q_atmin = false, q_pend = false;  // cur >= maxReplicas, cur <= minReplicas, pending pods
   const int wl = __popc(dnmask);  // down window: the last wl records
 
   auto refresh_J = [&](int rh) {
@@ -1299,6 +1300,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             q_mode = met ? (q_dreq < (1 << 24) ? 0 : 2) : (dnm == replicas ? 1 : 2);
           }
           q_unr = replicas > rpods;
+          q_atmax = replicas >= mx;
+          q_atmin = replicas <= minr;
+          q_pend = replicas > rpods;
           if constexpr (BDEF) {  // newest history record >= the new replica count
             int hit = -0x40000000;
 #pragma unroll
@@ -1306,7 +1310,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               const int e = (int)(short)(hdn[k >> 1] >> (16 * (k & 1)));
               hit = e >= replicas ? t - k : hit;
             }
-            q_hit = hit;
+            q_hold = hit + wl;
           }
         }
         // first step that needs the event path again: a node becomes ready,
@@ -1376,7 +1380,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       // a lane still stepping in sub-step `sub` has advanced in every earlier one
       const int L = Lpf[sub];
       int4 rec;
-      stall = t >= nxt;
       if constexpr (BDEF && D1_LEAN_V) {
         // Upstream default behavior, decided without the general path:
         // keep (util inside the tolerance band) leaves the replicas; a
@@ -1387,7 +1390,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // 24-bit products; anything outside their exact range, the unready
         // rule, an exact-multiple proposal (binary64 in the spec) or any
         // replica change is an event.
-        if (!stall) {
+        {
           const int cur = replicas;
           const int usage = min(L, q_rcap);
           const int a = (int)__umul24((uint32_t)usage, 100u);
@@ -1395,7 +1398,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           const int ra = a - (int)__umul24((uint32_t)util, (uint32_t)q_dreq);
           util += (ra >= q_dreq ? 1 : 0) - (ra < 0 ? 1 : 0);
           // unready pods and util above target: every replica counted, unready ones idle
-          const bool unr_up = q_unr && util > target;
+          const bool unr_up = q_unr & (util > target);
           int u = util, base = rpods;
           if (unr_up) {
             int nu = (int)((float)a * q_rbc);
@@ -1404,43 +1407,42 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             u = nu;
             base = cur;
           }
-          const bool keep = (uint32_t)(u - ulo) <= (uint32_t)(uhi - ulo) || (unr_up && u < target);
+          const bool keep = ((uint32_t)(u - ulo) <= (uint32_t)(uhi - ulo)) | (unr_up & (u < target));
           const int x = (int)__umul24((uint32_t)u, (uint32_t)base);
           int c = (int)((float)x * rtarget);
           int rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
           c += (rc >= target ? 1 : 0) - (rc < 0 ? 1 : 0);
           rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
           const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
-          const bool bad = met && ((uint32_t)usage >= (1u << 20) || (uint32_t)util >= (1u << 16) ||
-                                   (uint32_t)u >= (1u << 16) || (uint32_t)rc >= (uint32_t)target ||
-                                   (unr_up && q_dcur >= (1 << 24)));
-          if (__builtin_expect(met && !bad && !keep && rc == 0, 0))  // binary64 as the spec writes it
+          const bool bad = met & (((uint32_t)usage >= (1u << 20)) | ((uint32_t)util >= (1u << 16)) |
+                                  ((uint32_t)u >= (1u << 16)) | ((uint32_t)rc >= (uint32_t)target) |
+                                  (unr_up & (q_dcur >= (1 << 24))));
+          if (__builtin_expect(met & !bad & !keep & (rc == 0), 0))  // binary64 as the spec writes it
             c = (int)ceil(((double)u / (double)target) * (double)base);
           else
             c += rc != 0 ? 1 : 0;
-          const int pr = met && !keep ? (unr_up ? max(cur, c) : c) : cur;
-          const bool hold = pr == cur || (pr > cur ? cur >= mx : (q_hit >= t - wl || cur <= minr));
-          stall = q_mode > 1 || bad || !hold;
+          const int pr = (met & !keep) ? (unr_up ? max(cur, c) : c) : cur;
+          const bool hold = (pr == cur) | ((pr > cur) & q_atmax) | ((pr < cur) & ((t <= q_hold) | q_atmin));
+          stall = (t >= nxt) | (q_mode > 1) | bad | !hold;
           if (!stall) {
             ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
-            q_hit = met && pr >= cur ? t : q_hit;
+            q_hold = (met & (pr >= cur)) ? t + wl : q_hold;
             int upp = (int)((float)usage * q_rbp);
             const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
             upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
             if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
             else e_hour += dyn_energy(upp);
-            const int pending = cur - rpods;
-            const bool slo_b = pending > 0 || (met && util > slo_util);
+            const bool slo_b = q_pend | (met & (util > slo_util));
             slo += slo_b ? 1 : 0;
-            const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
-            rec = make_int4(cur, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
+            rec = make_int4(cur, cur - rpods, (nsp & 0xFFFF) | nod << 16,
+                            0xFFFF | (int)((q_peak ? 1u : 0u) << 16) | (slo_b ? (8 << 16) : 0));
             adv = true;
             if (traj) d1_store_rec(tp, rec);
             tp += ls;
             ++t;
           }
         }
-      } else if (!stall) {
+      } else if (!(stall = t >= nxt)) {
         const HpaOut h = hpa_eval(L, replicas, rpods, q_rbd, q_rbc);
         stall = h.desired != replicas;
         if (!stall) {
