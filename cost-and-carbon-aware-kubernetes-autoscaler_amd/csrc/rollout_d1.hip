@@ -666,6 +666,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // ---- scheduler state ----
   int t = 0;      // this lane's next step
   int nxt = 0;    // first step that must take the event path (the first step always does)
+  int npb = 0;    // next peak-window boundary step (pswitch lanes)
   int tq = 0;     // steps [tq, t) were quiet: their per-step constants are added at the next flush
   bool stall = false;
   // per-step constants of the quiet steps since the last event (SEMANTICS §3.H)
@@ -723,6 +724,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       int4 rec;
       uint32_t flags = 0;
       bool g_acted = false, hchg = false, jchg = false;
+      uint32_t emp_e = 0, weou_e = 0;  // empty slots / WhenEmptyOrUnderutilized slots after disruption
       HpaOut hp{};
       if (ev) {
         stall = false;
@@ -969,6 +971,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
         for (int q = 0; q < MAXP; ++q)
           if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) weou |= pmask[q];
+        weou_e = weou;
         const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)));
         // DRIFT: ready replacements take over (G1); drifted ready nodes not yet
         // being replaced are drift candidates (G0)
@@ -1253,6 +1256,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           }
         }
 
+        emp_e = emp;
       }
       D1_STAMP(6);
       if (ev) {
@@ -1326,18 +1330,15 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           int nx = min(next_ready, t + 60 - minute % 60);
 #endif
           if (pswitch) {
-            const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;
-            nx = min(nx, t + min(dps, dpe));
+            if (t >= npb) {  // the next peak-window boundary
+              const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;
+              npb = t + min(dps, dpe);
+            }
+            nx = min(nx, npb);
           }
-          uint32_t em = 0;
-#pragma unroll
-          for (int n = MAXN - 1; n >= 0; --n) em = 2 * em + (spods[n] == 0 ? 1u : 0u);
-          em &= used;
-          uint32_t wq = 0;
-#pragma unroll
-          for (int q = 0; q < MAXP; ++q)
-            if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) wq |= pmask[q];
-          const uint32_t gm = rdy & (em | (Ffree >= minscap ? wq : (wq & ~cmask)));
+          // empty slots and WhenEmptyOrUnderutilized pools as the disruption
+          // phase left them (deletions only clear bits that rdy clears too)
+          const uint32_t gm = rdy & (emp_e | (Ffree >= minscap ? weou_e : (weou_e & ~cmask)));
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) nx = ((gm >> n & 1u) && slc[n] > t) ? min(nx, slc[n]) : nx;
           if (g_acted || (ablate & 15)) nx = t + 1;  // ablation runs: every step an event
