@@ -312,7 +312,7 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_RB_V 64
 #endif
 #ifndef D1_K_V
-#define D1_K_V 4
+#define D1_K_V 2
 #endif
 #ifndef D1_VMN_V
 #define D1_VMN_V 12
@@ -324,10 +324,10 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_LAG_V 0
 #endif
 #ifndef D1_S_V
-#define D1_S_V 3
+#define D1_S_V 4
 #endif
 constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
-constexpr int D1_K = D1_K_V;      // event cadence and DMA batch (iterations, power of two)
+constexpr int D1_K = D1_K_V;      // event cadence (iterations)
 constexpr int D1_VMN = D1_VMN_V;  // rows in flight (vmcnt bound; <= 63)
 constexpr int D1_S = D1_S_V;      // quiet steps per iteration and lane
 static_assert(D1_VMN + 8 * D1_S <= D1_RB, "ring too small for the DMA lead");
@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     // its event step straight into quiet steps ----
     const uint64_t sb = __ballot(stall);
     if constexpr (STAMPS) st_acc[9] += 1;
-    if (sb != 0 && ((it & (D1_K - 1)) == D1_K - 1 || !qadv)) {
+    if (sb != 0 && (it % D1_K == D1_K - 1 || !qadv)) {
       if constexpr (STAMPS) { st_acc[10] += 1; st_acc[11] += __popcll(sb); }
       // the event step in phases, each a block over the stalled lanes (the
       // wave-uniform points between them carry the diagnostic stamps)
