@@ -61,6 +61,9 @@ struct ccka_ctx {
   ccka_traj_rec* d_traj = nullptr;
   int64_t traj_count = 0;
   bool traj_valid = false;
+  bool traj_nt = false;              // device records are [N][T] (single-deployment engine)
+  ccka_traj_rec* d_traj_t = nullptr;  // [T][N] copy for ccka_get_trajectory
+  int64_t traj_t_count = 0;
   void* d_parts = nullptr;
   ccka_totals* d_totals = nullptr;
   int32_t* d_sinq = nullptr;
@@ -483,6 +486,8 @@ int ccka_open(ccka_ctx** out, int device_ordinal) {
 static void free_results(ccka_ctx* c) {
   dfree(c->d_res);
   dfree(c->d_traj);
+  dfree(c->d_traj_t);
+  c->traj_t_count = 0;
   dfree(c->d_parts);
   dfree(c->d_detail);
   c->traj_count = 0;
@@ -956,12 +961,14 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     HIPCHK(c, launch_rollout_d1(p, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_engine = 2;
+    c->traj_nt = true;
   } else {
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
     HIPCHK(c, launch_rollout(k, block, lds, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_engine = 1;
+    c->traj_nt = false;
   }
   c->traj_valid = trajectory != 0;
   c->detail_valid = c->detail_on;
@@ -1116,6 +1123,7 @@ int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
   k.t1 = T;
   k.state_load = 0;
   c->last_engine = 3;
+  c->traj_nt = false;
   c->traj_valid = trajectory != 0;
   c->detail_valid = c->detail_on;
   c->pol_rec_valid = record != 0;
@@ -1183,7 +1191,19 @@ int ccka_get_trajectory(ccka_ctx* c, ccka_traj_rec* out, int64_t count) {
   if (!c->traj_valid) return fail(c, CCKA_ESTATE, "last rollout had no trajectory");
   if (count != c->traj_count) return fail(c, CCKA_EINVAL, "trajectory count mismatch");
   (void)hipSetDevice(c->device);
-  HIPCHK(c, hipMemcpyAsync(out, c->d_traj, (size_t)count * sizeof(ccka_traj_rec), hipMemcpyDeviceToHost, c->stream));
+  const ccka_traj_rec* src = c->d_traj;
+  if (c->traj_nt) {  // the single-deployment engine writes [N][T]: transpose on the device
+    if (c->traj_t_count != count) {
+      dfree(c->d_traj_t);
+      c->traj_t_count = 0;
+      if (hipMalloc((void**)&c->d_traj_t, (size_t)count * sizeof(ccka_traj_rec)) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "trajectory transpose alloc");
+      c->traj_t_count = count;
+    }
+    HIPCHK(c, launch_traj_transpose(c->d_traj, c->d_traj_t, c->N, count / c->N, c->stream));
+    src = c->d_traj_t;
+  }
+  HIPCHK(c, hipMemcpyAsync(out, src, (size_t)count * sizeof(ccka_traj_rec), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return CCKA_OK;
 }

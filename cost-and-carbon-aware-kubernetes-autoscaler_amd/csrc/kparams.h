@@ -261,5 +261,7 @@ hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipS
 hipError_t launch_policy_act(const float* y, int16_t* target, double* cw, int16_t* rec_target, double* rec_cw,
                              int64_t n, hipStream_t s);
 hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s);
+// [N][T] (single-deployment engine, device side) -> [T][N] (ccka_traj_rec order of the ABI)
+hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, hipStream_t s);
 
 }  // namespace ccka

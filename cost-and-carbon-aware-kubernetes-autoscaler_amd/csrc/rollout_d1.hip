@@ -701,7 +701,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int Lpf[D1_S];
 #pragma unroll
   for (int q = 0; q < D1_S; ++q) Lpf[q] = 0;
-  GLOBAL_AS int4* tp = traj + i;  // this lane's record of step t
+  // trajectory records scenario-major on the device ([N][T]: a lane's records
+  // are contiguous, so its consecutive steps fill whole lines however far the
+  // lanes drift apart); ccka_get_trajectory returns them [T][N]
+  GLOBAL_AS int4* tp = traj + i * (int64_t)T;  // this lane's record of step t
 
   for (int it = 0;; ++it) {
     const bool live = t < T;
@@ -1347,7 +1350,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       }
       if (ev) {
         if (traj) d1_store_rec(tp, rec);
-        tp += ls;
+        ++tp;
         ++t;
       }
       pf_ok = pf_ok && !ev;
@@ -1439,7 +1442,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                             0xFFFF | (int)((q_peak ? 1u : 0u) << 16) | (slo_b ? (8 << 16) : 0));
             adv = true;
             if (traj) d1_store_rec(tp, rec);
-            tp += ls;
+            ++tp;
             ++t;
           }
         }
@@ -1458,7 +1461,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           rec = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
           adv = true;
           if (traj) d1_store_rec(tp, rec);
-          tp += ls;
+          ++tp;
           ++t;
         }
       }
@@ -1497,6 +1500,34 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   p.final_nodes[i] = __popc(used);
   p.last_choice[i] = last_choice;
   p.hash[i] = hash;
+}
+
+// [N][T] -> [T][N] trajectory records (ccka_get_trajectory after the
+// single-deployment engine): 32 x 32 tiles through LDS, 16-byte elements,
+// both sides coalesced.
+__global__ void __launch_bounds__(256) traj_transpose_kernel(const int4* __restrict__ in, int4* __restrict__ out,
+                                                             int64_t N, int64_t T) {
+  __shared__ int4 tile[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const int64_t t0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int64_t n = n0 + ty + k, t = t0 + tx;
+    if (n < N && t < T) tile[ty + k][tx] = in[n * T + t];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const int64_t t = t0 + ty + k, n = n0 + tx;
+    if (n < N && t < T) out[t * N + n] = tile[tx][ty + k];
+  }
+}
+
+hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, hipStream_t s) {
+  const dim3 grid((unsigned)((T + 31) / 32), (unsigned)((N + 31) / 32));
+  hipLaunchKernelGGL(traj_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const int4*>(in),
+                     reinterpret_cast<int4*>(out), N, T);
+  return hipGetLastError();
 }
 
 hipError_t launch_table(const TableParams& t, hipStream_t s) {
