@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int ps = opq(p.peak_start) % 1440, pe = opq(p.peak_end) % 1440;
   const int ps_raw = opq(p.peak_start), pe_raw = opq(p.peak_end);
   const int sm0 = opq(p.start_minute) % 1440;
-  const long long base_nw = opq(p.base_nw), ls = opq(p.N);
+  const long long base_nw = opq(p.base_nw);
   const GLOBAL_AS int32_t* const price = opq_ptr(p.price);
   const GLOBAL_AS double* const ci_gpwmin = opq_ptr(p.ci_gpwmin);
   const GLOBAL_AS int2* const table = opq_ptr(p.table);
@@ -522,7 +522,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int q_mode = 2;               // 0: metric (ready*req < 2^24), 1: no metric and replicas in range, 2: events only
   bool q_unr = false;           // unready pods
   int q_hold = -0x40000000;     // the down window holds a record >= cur up to this step
-  bool q_atmax = false, q_atmin = false, q_pend = false;  // cur >= maxReplicas, cur <= minReplicas, pending pods
+  bool q_atmax = false, q_pend = false;  // cur >= maxReplicas, pending pods
+  int q_umax = -1;  // largest usage the quiet step evaluates exactly (-1: every step is an event)
   const int wl = __popc(dnmask);  // down window: the last wl records
 
   auto refresh_J = [&](int rh) {
@@ -1308,7 +1309,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           }
           q_unr = replicas > rpods;
           q_atmax = replicas >= mx;
-          q_atmin = replicas <= minr;
           q_pend = replicas > rpods;
           if constexpr (BDEF) {  // newest history record >= the new replica count
             int hit = -0x40000000;
@@ -1317,7 +1317,19 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               const int e = (int)(short)(hdn[k >> 1] >> (16 * (k & 1)));
               hit = e >= replicas ? t - k : hit;
             }
-            q_hold = hit + wl;
+            q_hold = replicas <= minr ? 0x3fffffff : hit + wl;
+          }
+          // Exactness range of the quiet step's arithmetic: usage < 2^20 (f32
+          // exact), util < 2^16 (usage*100 < 2^16*ready*req), and proposal
+          // estimates u*base/target < 2^20 for u < 2^16 (base < 16*target), so
+          // every f32 quotient is within one of the truth and one remainder
+          // correction makes it exact. Outside it, or in mode 2, every step
+          // is an event (the general evaluation is exact everywhere).
+          {
+            const long long ucap = ((long long)q_dreq << 16) / 100;  // usage*100 < 2^16*dreq
+            const int base_max = q_unr ? max(replicas, rpods) : rpods;
+            const bool ok = q_mode < 2 && base_max < 16 * target && (!q_unr || q_dcur < (1 << 24));
+            q_umax = !ok ? -1 : (q_mode == 1 ? 0x7fffffff : (int)min(ucap - 1, (long long)(1 << 20) - 1));
           }
         }
         // first step that needs the event path again: a node becomes ready,
@@ -1418,19 +1430,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           c += (rc >= target ? 1 : 0) - (rc < 0 ? 1 : 0);
           rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
           const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
-          const bool bad = met & (((uint32_t)usage >= (1u << 20)) | ((uint32_t)util >= (1u << 16)) |
-                                  ((uint32_t)u >= (1u << 16)) | ((uint32_t)rc >= (uint32_t)target) |
-                                  (unr_up & (q_dcur >= (1 << 24))));
+          // usage <= q_umax proves every estimate above exact (see the caches)
+          const bool bad = (uint32_t)usage > (uint32_t)q_umax;
           if (__builtin_expect(met & !bad & !keep & (rc == 0), 0))  // binary64 as the spec writes it
             c = (int)ceil(((double)u / (double)target) * (double)base);
           else
             c += rc != 0 ? 1 : 0;
           const int pr = (met & !keep) ? (unr_up ? max(cur, c) : c) : cur;
-          const bool hold = (pr == cur) | ((pr > cur) & q_atmax) | ((pr < cur) & ((t <= q_hold) | q_atmin));
-          stall = (t >= nxt) | (q_mode > 1) | bad | !hold;
+          // above cur: held at maxReplicas; below: held while the down window
+          // has a record >= cur (q_hold, unbounded at minReplicas)
+          const bool hold = ((pr <= cur) | q_atmax) & ((pr >= cur) | (t <= q_hold));
+          stall = (t >= nxt) | bad | !hold;
           if (!stall) {
             ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
-            q_hold = (met & (pr >= cur)) ? t + wl : q_hold;
+            q_hold = (met & (pr >= cur)) ? max(q_hold, t + wl) : q_hold;
             int upp = (int)((float)usage * q_rbp);
             const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
             upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
