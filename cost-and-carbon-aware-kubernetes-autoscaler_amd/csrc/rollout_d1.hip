@@ -1432,10 +1432,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
           // usage <= q_umax proves every estimate above exact (see the caches)
           const bool bad = (uint32_t)usage > (uint32_t)q_umax;
+          c += rc != 0 ? 1 : 0;
           if (__builtin_expect(met & !bad & !keep & (rc == 0), 0))  // binary64 as the spec writes it
             c = (int)ceil(((double)u / (double)target) * (double)base);
-          else
-            c += rc != 0 ? 1 : 0;
           const int pr = (met & !keep) ? (unr_up ? max(cur, c) : c) : cur;
           // above cur: held at maxReplicas; below: held while the down window
           // has a record >= cur (q_hold, unbounded at minReplicas)
@@ -1447,8 +1446,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             int upp = (int)((float)usage * q_rbp);
             const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
             upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
-            if ((float)upp * Rmax < 0.9999f) e_hour += (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-            else e_hour += dyn_energy(upp);
+            long long ed = (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+            if (__builtin_expect(!((float)upp * Rmax < 0.9999f), 0)) ed = dyn_energy(upp);  // a node saturates
+            e_hour += ed;
             const bool slo_b = q_pend | (met & (util > slo_util));
             slo += slo_b ? 1 : 0;
             rec = make_int4(cur, cur - rpods, (nsp & 0xFFFF) | nod << 16,
