@@ -369,6 +369,12 @@ __device__ __forceinline__ void d1_wait_rows() {
 }
 __device__ __forceinline__ void d1_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// logical block of dispatch block b among n (a bijection; 8 XCDs)
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7u, k = b >> 3, q = n >> 3, r = n & 7u;
+  return x * q + min(x, r) + k;
+}
+
 template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -383,7 +389,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   __syncthreads();
   // lanes-per-wave mapping: wave w owns scenarios [w*lpw, (w+1)*lpw)
   const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
+  // XCD-aware block order: blocks are dealt round-robin to the 8 XCDs, so
+  // block b takes the (b / 8)-th block of XCD b % 8's contiguous scenario
+  // range; trace rows shared by neighbouring blocks then sit in one XCD's L2
+  // (one HBM fetch) instead of two
+  const int64_t wv = (int64_t)xcd_block(blockIdx.x, gridDim.x) * (blockDim.x / WAVE) + (threadIdx.x / WAVE);
   const int64_t i = wv * p.lpw + lane;
   if (lane >= p.lpw || i >= p.N) return;  // no cross-lane operations below but ballots
 
