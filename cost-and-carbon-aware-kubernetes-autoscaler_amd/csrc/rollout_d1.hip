@@ -285,23 +285,24 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
   }
 
 // ---------------------------------------------------------------------------
-// Lane-skewed schedule (docs/DESIGN.md "rollout_d1_kernel"):
+// Lane-skewed schedule (DESIGN.md "rollout_d1_kernel"):
 // every lane (scenario) keeps its own step counter. Most lane-steps are
 // quiet: the HPA keeps the replica count (desired == current, including the
 // steps the stabilisation window or maxReplicas hold it) and no node becomes
-// ready, no hour / profile boundary is crossed and no node becomes a new
+// ready, no hour / peak-window boundary is crossed and no node becomes a new
 // consolidation candidate. A quiet step is the HPA evaluation, the history
-// push, the step's energy from cached sums and the trajectory record. Any
-// other step is an event: the lane stalls and the wave runs the full step
-// for all stalled lanes together every D1_K iterations, so the long event
-// path runs once for many lanes instead of once per step for the union of
-// every lane's events. Per-step constants (node cost, idle energy, pending
+// push, the step's energy from cached sums and the trajectory record; a lane
+// takes up to D1_S of them per iteration. Any other step is an event: the
+// lane stalls and every D1_K iterations the wave runs the full step for all
+// stalled lanes together (before that iteration's quiet steps), so the long
+// event path runs once for many lanes instead of once per step for the union
+// of every lane's events. Per-step constants (node cost, idle energy, pending
 // pods, node-minutes) are added lazily at the next event.
 //
 // Load samples reach the lanes through a per-wave LDS ring of D1_RB trace
 // rows (row t, lane l at [t % D1_RB][l]) filled by LDS-DMA
-// (global_load_lds_dword, one row = the wave's scenarios at one step) D1_K
-// rows every D1_K iterations, far ahead of the lanes; a row is read only
+// (global_load_lds_dword, one row = the wave's scenarios at one step), D1_S
+// rows per iteration and D1_VMN rows ahead of the lanes; a row is read only
 // after D1_VMN younger DMA instructions were issued and `s_waitcnt
 // vmcnt(D1_VMN)` retired it (every DMA instruction is one consecutive row).
 // The ring is refilled only when every live lane has consumed the rows it
@@ -320,9 +321,6 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #ifndef D1_LEAN_V
 #define D1_LEAN_V 1
 #endif
-#ifndef D1_LAG_V
-#define D1_LAG_V 0
-#endif
 #ifndef D1_S_V
 #define D1_S_V 4
 #endif
@@ -337,10 +335,13 @@ constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
 #ifndef D1_NT_V
 #define D1_NT_V 0
 #endif
-#if D1_NT_V
-#define D1_NT " nt"
+#ifndef D1_NTL_V
+#define D1_NTL_V 0
+#endif
+#if D1_NTL_V
+#define D1_NTL " nt"
 #else
-#define D1_NT ""
+#define D1_NTL ""
 #endif
 __device__ __forceinline__ void d1_store_rec(GLOBAL_AS int4* p, const int4& v) {
 #if D1_NT_V
@@ -358,7 +359,7 @@ __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row)
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, off" D1_NT "\n\t"
+      "global_load_lds_dword %1, off" D1_NTL "\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(src), "s"(lds_row)
@@ -1349,11 +1350,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // with the same candidates), or the next step when disruption acted
         // (the budget may allow more)
         {
-#ifdef D1_NOHOUR_TEST
-          int nx = next_ready;  // timing experiment only (wrong results)
-#else
           int nx = min(next_ready, t + 60 - minute % 60);
-#endif
           if (pswitch) {
             if (t >= npb) {  // the next peak-window boundary
               const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;

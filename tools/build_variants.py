@@ -1,7 +1,9 @@
-"""Build-time variants of the single-deployment kernel (D1_V_* macros in
-rollout_d1.hip) as separate libccka.so copies under csrc/build/variants/<name>/,
+"""Build-time variants of the single-deployment kernel (D1_*_V macros in
+rollout_d1.hip: D1_S_V quiet steps per iteration, D1_K_V event cadence,
+D1_VMN_V trace rows in flight, D1_LEAN_V default-behavior quiet path, D1_NT_V /
+D1_NTL_V streaming hints) as separate libccka.so copies under csrc/build/variants/<name>/,
 linked with the main build's other objects. Profiling aid only.
-usage: python tools/build_variants.py name=-DD1_V_ACC=1 [name2="-DA -DB" ...]"""
+usage: python tools/build_variants.py name=-DD1_S_V=3 [name2="-DA -DB" ...]"""
 import os
 import subprocess
 import sys
