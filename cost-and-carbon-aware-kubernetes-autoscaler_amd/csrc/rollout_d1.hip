@@ -702,9 +702,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const uint32_t ring_lds = (uint32_t)(uintptr_t)s_acc + ring_off;
   const int* const ring = reinterpret_cast<const int*>(reinterpret_cast<const char*>(s_acc) + ring_off);
   int tf = 0;  // trace rows issued (wave-uniform)
+  const int32_t* lpf = lp;  // this lane's sample of row tf
   {
     const int n0 = min(T, D1_VMN + 4 * D1_S);
-    for (; tf < n0; ++tf) d1_dma_row(lp + (int64_t)tf * lsl, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
+    for (; tf < n0; ++tf, lpf += lsl) d1_dma_row(lpf, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
     d1_wait_all();
   }
   int t_rdy = tf;  // rows < t_rdy have landed (wave-uniform)
@@ -1309,9 +1310,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         {
           q_rbd = __builtin_amdgcn_rcpf((float)(rpods * req));
           q_rbc = __builtin_amdgcn_rcpf((float)(replicas * req));
-          q_rcap = limit > 0 ? rpods * limit : 0x7fffffff;
-          q_dreq = rpods * req;
-          q_dcur = replicas * req;
+          // (rpods, replicas <= 32767 and req, limit <= 65535: exact 24-bit products)
+          q_rcap = limit > 0 ? (int)__umul24((uint32_t)rpods, (uint32_t)limit) : 0x7fffffff;
+          q_dreq = (int)__umul24((uint32_t)rpods, (uint32_t)req);
+          q_dcur = (int)__umul24((uint32_t)replicas, (uint32_t)req);
           {
             const bool met = replicas <= mx && replicas >= minr && rpods > 0 && !(replicas == 0 && minr != 0);
             const bool hpa_path = !(replicas == 0 && minr != 0);
@@ -1337,10 +1339,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           // correction makes it exact. Outside it, or in mode 2, every step
           // is an event (the general evaluation is exact everywhere).
           {
-            const long long ucap = ((long long)q_dreq << 16) / 100;  // usage*100 < 2^16*dreq
+            // usage*100 < 2^16*dreq, from below: 655.35 < 2^16/100 and f32 rounding
+            // (< 2^-23 relative) cannot reach the 1.5e-5 margin
+            const int ucap = (int)fminf((float)q_dreq * 655.35f, 1048575.0f);
             const int base_max = q_unr ? max(replicas, rpods) : rpods;
             const bool ok = q_mode < 2 && base_max < 16 * target && (!q_unr || q_dcur < (1 << 24));
-            q_umax = !ok ? -1 : (q_mode == 1 ? 0x7fffffff : (int)min(ucap - 1, (long long)(1 << 20) - 1));
+            q_umax = !ok ? -1 : (q_mode == 1 ? 0x7fffffff : ucap);
           }
         }
         // first step that needs the event path again: a node becomes ready,
@@ -1382,7 +1386,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       if (__ballot(t < T && t < tf + D1_S - D1_RB) == 0) {
         const int n1 = min(T, tf + D1_S);
         for (; tf < n1; ++tf)
-          d1_dma_row(lp + (int64_t)tf * lsl, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
+          d1_dma_row(lpf, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4)), lpf += lsl;
         if (tf == T) {  // no younger DMA will retire the last rows
           d1_wait_all();
           t_rdy = T;
