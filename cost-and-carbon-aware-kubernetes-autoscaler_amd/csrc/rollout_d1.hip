@@ -1450,15 +1450,18 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           // above cur: held at maxReplicas; below: held while the down window
           // has a record >= cur (q_hold, unbounded at minReplicas)
           const bool hold = ((pr <= cur) | q_atmax) & ((pr >= cur) | (t <= q_hold));
+          // the step's energy: independent of the HPA chain above (interleaves with it)
+          int upp = (int)((float)usage * q_rbp);
+          const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
+          upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
+          const bool sat = !((float)upp * Rmax < 0.9999f);
+          const long long edq = (long long)(Ssum * (unsigned long long)(uint32_t)upp);
           stall = (t >= nxt) | bad | !hold;
           if (!stall) {
             ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
             q_hold = (met & (pr >= cur)) ? max(q_hold, t + wl) : q_hold;
-            int upp = (int)((float)usage * q_rbp);
-            const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
-            upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
-            long long ed = (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-            if (__builtin_expect(!((float)upp * Rmax < 0.9999f), 0)) ed = dyn_energy(upp);  // a node saturates
+            long long ed = edq;
+            if (__builtin_expect(sat, 0)) ed = dyn_energy(upp);  // a node saturates
             e_hour += ed;
             const bool slo_b = q_pend | (met & (util > slo_util));
             slo += slo_b ? 1 : 0;
