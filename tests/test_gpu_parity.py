@@ -258,6 +258,55 @@ def test_d1_edge_cases(engine, variant):
     compare(rg, rc, tg, tc)
 
 
+@pytest.mark.parametrize("lpw,steps", [(1, 97), (7, 5), (17, 29), (33, 1440), (64, 300), (49, 61)])
+def test_d1_lane_skew_schedule(engine, lpw, steps):
+    """The lane-skewed schedule of rollout_d1_kernel (quiet steps per lane,
+    batched event steps, LDS-DMA trace ring, scenario-major records): any
+    scenarios per wave (one lane to a full wave, partial last waves) and
+    horizons shorter than the ring prologue, not a multiple of the quiet
+    steps per iteration, or the full day, bit-exact against the oracle."""
+    import ctypes as C
+
+    spec = configs.config2_world(n_steps=steps)
+    n = 997
+    sc = configs.hpa_scenarios(n, 11)
+    load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=11)
+    engine.lib.ccka_debug_lpw.argtypes = [C.c_void_p, C.c_int32]
+    assert engine.lib.ccka_debug_lpw(engine.ctx, lpw) == 0
+    try:
+        rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    finally:
+        engine.lib.ccka_debug_lpw(engine.ctx, 0)
+    assert engine.last_engine()[0] == 2
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
+
+
+@pytest.mark.parametrize("variant", ["start_37", "peak_odd_wrap", "peak_empty", "no_switch"])
+def test_d1_boundaries_off_the_hour(engine, variant):
+    """Hour and peak-window boundaries that do not coincide (the next-event
+    step of a lane is the minimum of both), a wrapped window, an empty one."""
+    spec = configs.config2_world(n_steps=700)
+    n = 600
+    sc = configs.hpa_scenarios(n, 3)
+    load = po.gen_load(configs.trace_gen(5), spec.n_steps, 1, n, first_id=3)
+    if variant == "start_37":
+        spec.start_minute = 37
+        spec.peak_start, spec.peak_end = 300, 420
+    elif variant == "peak_odd_wrap":
+        spec.start_minute = 1200
+        spec.peak_start, spec.peak_end = 1301, 97
+    elif variant == "peak_empty":
+        spec.peak_start = spec.peak_end = 611
+    elif variant == "no_switch":
+        spec.peak_switch = 0
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2, variant
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert (tc["flags"] & 1).any() == (variant != "peak_empty" and variant != "no_switch")
+    compare(rg, rc, tg, tc)
+
+
 def test_d1_matches_general_kernel(engine):
     spec = configs.config3_world(n_steps=360)
     n = 1500
