@@ -93,6 +93,9 @@ struct ccka_ctx {
   uint8_t* d_wci = nullptr;
   int2* d_table = nullptr;
   int32_t* d_jtab = nullptr;
+  int2* d_table2 = nullptr;   // G2 offer table (replacement consolidation in the single-deployment kernel)
+  int32_t* d_jtab2 = nullptr;
+  double* d_wc0 = nullptr;    // one zero carbon weight (the offer table's score is the price)
   int JT = 0, NW = 0;
   int engine_mode = 0;       // 0 auto, 1 general kernel only (ccka_debug_engine)
   unsigned long long* d_stamps = nullptr;
@@ -364,16 +367,17 @@ static bool d1_drift_inert(const ccka_ctx* c) {
   return !switching || same;
 }
 
-// The single-deployment kernel runs drift itself (8 slots, <= 2 pools: its
-// DRIFT instantiation, SEMANTICS 3.G0); replacement and multi-node
-// consolidation run on the general kernel unless provably inert:
-//  - replacement needs an on-demand node in a WhenEmptyOrUnderutilized pool:
-//    never when no pool profile uses that policy or no scenario's nodeSelector
-//    admits on-demand;
-//  - multi-node consolidation needs a WhenEmptyOrUnderutilized pool.
-static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift) {
+// The single-deployment kernel runs drift (SEMANTICS 3.G0) and single-node
+// replacement consolidation (3.G2) itself in its DRIFT instantiation (8
+// slots, <= 2 pools); multi-node consolidation runs on the general kernel
+// unless provably inert. Replacement needs an on-demand node in a
+// WhenEmptyOrUnderutilized pool: inert when no pool profile uses that policy
+// or no scenario's nodeSelector admits on-demand; multi-node consolidation
+// needs a WhenEmptyOrUnderutilized pool.
+static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace) {
   const ccka_world& w = c->hw;
   *drift = !d1_drift_inert(c);
+  *replace = false;
   if (*drift && !(w.max_nodes <= 8 && w.n_pools <= 2)) return false;
   bool weou = false;
   for (int q = 0; q < w.n_pools; ++q) {
@@ -382,7 +386,10 @@ static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift) {
   }
   if (w.disrupt_ext & CCKA_DISRUPT_REPLACE) {
     const uint32_t sel = c->sc_capsel_or ? c->sc_capsel_or : w.deploy[0].cap_sel;
-    if (weou && (sel & CCKA_CAP_OD)) return false;
+    if (weou && (sel & CCKA_CAP_OD)) {
+      if (!(w.max_nodes <= 8 && w.n_pools <= 2)) return false;
+      *replace = true;
+    }
   }
   if ((w.disrupt_ext & CCKA_DISRUPT_MULTI) && weou) return false;
   return true;
@@ -392,9 +399,11 @@ static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift) {
 static int d1_prepare(ccka_ctx* c) {
   c->d1_ready = true;
   c->d1_ok = false;
-  bool drift = false;
-  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_ok(c, &drift)) return CCKA_OK;
-  c->d1.drift = drift ? 1 : 0;
+  bool drift = false, replace = false;
+  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_ok(c, &drift, &replace)) return CCKA_OK;
+  c->d1.drift = (drift || replace) ? 1 : 0;  // the DRIFT instantiation carries both
+  c->d1.drift_on = drift ? 1 : 0;
+  c->d1.replace = replace ? 1 : 0;
   if (c->sc_dstab_max > CCKA_HIST * CCKA_STEP_SECONDS) return CCKA_OK;  // beyond the register ring
   const size_t n = (size_t)c->N;
   std::vector<double> wl;
@@ -426,9 +435,18 @@ static int d1_prepare(ccka_ctx* c) {
   const size_t keys = (size_t)w.n_regions * 24 * c->zmasks.size() * 3;
   dfree(c->d_table);
   dfree(c->d_jtab);
+  dfree(c->d_table2);
+  dfree(c->d_jtab2);
   if (hipMalloc((void**)&c->d_table, keys * c->NW * c->JT * sizeof(int2)) != hipSuccess ||
       hipMalloc((void**)&c->d_jtab, keys * sizeof(int32_t)) != hipSuccess)
     return fail(c, CCKA_ENOMEM, "argmin table alloc (%zu keys x %d weights x %d)", keys, c->NW, c->JT);
+  if (replace) {  // the G2 offer table: cheapest offering holding n pods, by price
+    const double zero = 0.0;
+    if ((rc = dupload(c, c->d_wc0, &zero, 1)) != CCKA_OK) return rc;
+    if (hipMalloc((void**)&c->d_table2, keys * c->JT * sizeof(int2)) != hipSuccess ||
+        hipMalloc((void**)&c->d_jtab2, keys * sizeof(int32_t)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "offer table alloc (%zu keys x %d)", keys, c->JT);
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->d1_ok = true;
   return CCKA_OK;
@@ -507,6 +525,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_sinq);
   dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
+  dfree(c->d_table2); dfree(c->d_jtab2); dfree(c->d_wc0);
   dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_ggather); dfree(c->d_gcounts); dfree(c->d_gn);
   dfree(c->d_gflags); dfree(c->d_gfront); dfree(c->d_hist);
   dfree(c->d_pol_state); dfree(c->d_pol_target); dfree(c->d_pol_cw); dfree(c->d_rec_target); dfree(c->d_rec_cw);
@@ -957,6 +976,17 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_table(tp, c->stream));
+    p.table2 = nullptr;
+    if (p.replace) {  // the G2 offer table (price only)
+      TableParams t2 = tp;
+      t2.wc1000 = c->d_wc0;
+      t2.NW = 1;
+      t2.offer = 1;
+      t2.table = c->d_table2;
+      t2.jtab = c->d_jtab2;
+      HIPCHK(c, launch_table(t2, c->stream));
+      p.table2 = c->d_table2;
+    }
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
     HIPCHK(c, launch_rollout_d1(p, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));

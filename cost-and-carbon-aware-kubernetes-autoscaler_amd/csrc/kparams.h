@@ -201,8 +201,11 @@ struct D1Params {
   D1Rule up, dn;
   int32_t budget[CCKA_MAX_POOLS];
   D1Patch patch[CCKA_MAX_POOLS][4];  // base, RESET, OFFPEAK, PEAK
-  int32_t drift;                     // 1: Karpenter drift (SEMANTICS 3.G0) in the kernel
+  int32_t drift;                     // 1: the DRIFT instantiation (drift and/or replacement)
   uint32_t zml[16];                  // zone mask of each zone-mask index (patch zi)
+  int32_t drift_on;                  // 1: Karpenter drift (SEMANTICS 3.G0) acts
+  int32_t replace;                   // 1: replacement consolidation offers (SEMANTICS 3.G2)
+  const int2* table2;                // [R][24][NZI][3][JT] cheapest offering by price (the G2 offer rule)
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)
@@ -217,6 +220,7 @@ struct TableParams {
   int2* table;
   int32_t* jtab;
   int32_t K, Z, R, NZI, NW, JT;
+  int32_t offer;  // 1: the G2 offer rule (price only, no spot-first preference; NW = 1)
 };
 
 hipError_t launch_table(const TableParams& t, hipStream_t s);

@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) table_kernel(TableParams q) {
   const int zi = (int)(x % q.NZI); x /= q.NZI;
   const int rh = (int)x;  // r * 24 + h
   const uint32_t cm = (uint32_t)cmi + 1u, zm = q.zmasks[zi];
-  const double wc = q.wc1000[wi];
+  const double wc = q.offer ? 0.0 : q.wc1000[wi];
   const double ci = q.ci_gpwh[rh];
   const int32_t* tile = q.price + (int64_t)rh * q.K * q.Z * 2;
   int2* out = q.table + key * q.JT;
@@ -139,7 +139,9 @@ __global__ void __launch_bounds__(256) table_kernel(TableParams q) {
     take_if_better(bs, cs);
     take_if_better(ba, ca);
     if (v && c1 > c1n) {
-      const Best& w = bs.info >= 0 ? bs : ba;  // spot first when any spot offering holds n
+      // spot first when any spot offering holds n (the F launch rule); the
+      // G2 offer rule takes the cheapest of all
+      const Best& w = (!q.offer && bs.info >= 0) ? bs : ba;
       const int info = w.info >= 0 ? (w.info | c1 << 16) : -1;
       const int hi = min(c1, q.JT - 1);
       for (int n = c1n + 1; n <= hi; ++n) out[n] = make_int2(w.price, info);
@@ -428,6 +430,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const GLOBAL_AS int32_t* const price = opq_ptr(p.price);
   const GLOBAL_AS double* const ci_gpwmin = opq_ptr(p.ci_gpwmin);
   const GLOBAL_AS int2* const table = opq_ptr(p.table);
+  const GLOBAL_AS int2* const table2 = opq_ptr(p.table2);
+  const int drift_on = opq(p.drift_on), replace = opq(p.replace);
   const GLOBAL_AS int32_t* const jtab = opq_ptr(p.jtab);
   GLOBAL_AS int4* const traj = opq_ptr(reinterpret_cast<int4*>(p.traj));
   // BDEF: the upstream default behavior as compile-time constants
@@ -495,6 +499,13 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // 1 + slot in sinfo bits 16..20)
   uint32_t dmask = 0, srcm = 0, repm = 0;
   auto taint = [&]() -> uint32_t { return DRIFT ? (srcm | repm) : 0u; };
+  // slots of on-demand nodes (G2 candidates are on-demand)
+  auto od_slots = [&]() {
+    uint32_t m = 0;
+#pragma unroll
+    for (int n = MAXN - 1; n >= 0; --n) m = 2 * m + (sinfo[n] >> 12 & 1u);
+    return m & used;
+  };
   const uint32_t slot_mask = maxn >= 32 ? 0xFFFFFFFFu : ((1u << maxn) - 1u);
 
   int replicas = p.replicas0, placed = 0, rpods = 0;
@@ -804,7 +815,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               scas[n] = c;
             }
           jchg = true;
-          if constexpr (DRIFT) {  // the pools' requirements moved: which nodes left them
+          if (DRIFT && drift_on) {  // the pools' requirements moved: which nodes left them
             uint32_t dm = 0;
 #pragma unroll
             for (int n = 0; n < MAXN; ++n) {
@@ -988,7 +999,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         for (int q = 0; q < MAXP; ++q)
           if (q < NP && ppol[q] == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) weou |= pmask[q];
         weou_e = weou;
-        const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)));
+        // G2 (replacement consolidation): on-demand WEOU nodes with pods, not being replaced
+        const uint32_t g2c = (DRIFT && replace) ? (weou & od_slots() & ~emp & ~srcm) : 0u;
+        const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)) | g2c);
         // DRIFT: ready replacements take over (G1); drifted ready nodes not yet
         // being replaced are drift candidates (G0)
         const uint32_t tkm = DRIFT ? (repm & rdy) : 0u;
@@ -1263,6 +1276,81 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 emp = em & used;
               }
             }
+            if constexpr (DRIFT) {
+              // G2: the first candidate (pods asc, price desc, slot asc) with a
+              // strictly cheaper single offering for its pods gets a pre-spun
+              // replacement (the offer table: price only); one per pool per step
+              if (replace && weou_q && deleted < qbudget) {
+                uint32_t c2 = elig & pmask[q] & od_slots() & ~emp & ~srcm;
+                while (c2) {
+                  unsigned long long bkey = ~0ull;
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) {
+                    const unsigned long long key = (unsigned long long)spods[n] << 36 |
+                                                   (unsigned long long)(0x7fffffff - sprice[n]) << 4 | (unsigned)n;
+                    bkey = ((c2 >> n & 1u) && key < bkey) ? key : bkey;
+                  }
+                  const int best = (int)(bkey & 15u), bp = (int)(bkey >> 36);
+                  const int bpr = 0x7fffffff - (int)((bkey >> 4) & 0x7fffffffull);
+                  const uint32_t fr = ~used & slot_mask;
+                  if (!fr) break;  // no free slot: the search ends
+                  uint32_t cmq = 0;
+                  int zq = -1, cq = 0;
+#pragma unroll
+                  for (int qq = 0; qq < MAXP; ++qq)
+                    if (qq == q) { zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
+                  int2 e = make_int2(0, -1);
+                  if (!(pdb_member && bp > allowed) && cmq && zq >= 0)
+                    e = *(const int2*)(table2 + (((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * JT + bp);
+                  if (e.y < 0 || e.x >= bpr) {  // PDB, no offer or not strictly cheaper
+                    c2 &= ~(1u << best);
+                    continue;
+                  }
+                  const int info = e.y, prc = e.x;
+                  const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
+                  const int slot = __ffs((int)fr) - 1;
+                  const int rs = t + delay;
+                  const int4 ac = s_acc[bk];
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) {
+                    if (n == slot) {
+                      sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13 | (best + 1) << 16);
+                      sready[n] = rs;
+                      slc[n] = t + casc(cq);
+                      scas[n] = casc(cq);
+                      spods[n] = 0;
+                      sprice[n] = prc;
+                      scap[n] = cap1;
+                      sdyn[n] = (uint32_t)ac.z;
+                      salloc[n] = ac.w;
+                      sallocr[n] = delay == 0 ? ac.w : 0;
+                      sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
+                    }
+                  }
+                  const uint32_t bit = 1u << slot;
+                  used |= bit;
+                  if (capbit1(bc) & capsel) cmask |= bit;
+#pragma unroll
+                  for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
+                  if (delay == 0) rdy |= bit;
+                  else next_ready = min(next_ready, rs);
+                  minscap = min(minscap, cap1);
+                  Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
+                  if (bc == 0) nsp++; else nod++;
+                  burn += prc;
+                  launches++;
+                  last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+                  hash = (hash ^ last_choice) * 16777619u;
+                  step_last_type = bk;
+                  srcm |= 1u << best;
+                  repm |= bit;
+                  flags |= 2u | 32u;
+                  deleted++;
+                  g_acted = true;
+                  break;
+                }
+              }
+            }
           }
           if (any_del) {  // capacity of the remaining nodes
             g_acted = true;
@@ -1364,7 +1452,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           }
           // empty slots and WhenEmptyOrUnderutilized pools as the disruption
           // phase left them (deletions only clear bits that rdy clears too)
-          const uint32_t gm = rdy & (emp_e | (Ffree >= minscap ? weou_e : (weou_e & ~cmask)));
+          const uint32_t gm = rdy & (emp_e | (Ffree >= minscap ? weou_e : (weou_e & ~cmask)) |
+                                     ((DRIFT && replace) ? (weou_e & od_slots() & ~emp_e & ~srcm) : 0u));
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) nx = ((gm >> n & 1u) && slc[n] > t) ? min(nx, slc[n]) : nx;
           if (g_acted || (ablate & 15)) nx = t + 1;  // ablation runs: every step an event

@@ -483,7 +483,9 @@ def test_replacement_parity_single_deployment(engine, variant):
             p.limit_cpu_m = 12000
     load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=sc.first_id)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
-    assert engine.last_engine()[0] == 1
+    # replacement runs inside the single-deployment kernel (8 slots, <= 2 pools,
+    # no pool limits); pool limits take the general kernel
+    assert engine.last_engine()[0] == (1 if variant == "pool_limit" else 2), variant
     rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
     if variant != "pdb50":
         assert ((tc["flags"] & 32) != 0).any()  # replacements happened
@@ -512,14 +514,17 @@ def test_replacement_parity_multi_deployment(engine):
 
 
 def test_inert_disruption_runs_on_d1(engine):
-    """Worlds that enable drift / replacement where neither can ever act run on
-    the single-deployment kernel and still match the oracle (which runs the
-    phases); a world where they can act runs on the general kernel."""
+    """Worlds that enable drift / replacement run on the single-deployment
+    kernel within its 8 slots and 2 pools (inert or not) and match the oracle
+    (which runs the phases); beyond them they run on the general kernel."""
     spec = configs.config2_world(n_steps=1440)
     spec.replace = 1
     sc = configs.hpa_scenarios(1200)
-    run_engine(engine, spec, sc, load=po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n))
-    assert engine.last_engine()[0] == 1  # half the scenarios select on-demand: not inert
+    load = po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2  # half the scenarios select on-demand: replacement can act
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
     sc.cap_sel = np.full(sc.n, abi.CAP_SPOT, np.uint8)  # spot-only: no on-demand node can exist
     load = po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
