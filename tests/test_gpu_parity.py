@@ -492,6 +492,38 @@ def test_replacement_parity_single_deployment(engine, variant):
     compare(rg, rc, tg, tc)
 
 
+@pytest.mark.parametrize("lpw,steps,max_nodes,start", [(5, 300, 8, 0), (64, 1440, 8, 37), (23, 700, 3, 11),
+                                                     (40, 900, 2, 0)])
+def test_d1_replacement_schedule(engine, lpw, steps, max_nodes, start):
+    """Replacement consolidation (+ drift) inside the single-deployment kernel
+    under the lane-skewed schedule: offers re-evaluated only at event steps
+    (hour boundaries off the clock hour, readiness, scheduling), few or no
+    free slots for the replacement, bit-exact against the oracle."""
+    import ctypes as C
+
+    spec = configs.config2_world(n_steps=steps, max_nodes=max_nodes)
+    spec.replace = 1
+    spec.drift = 1
+    spec.pdb_pct = -1
+    spec.start_minute = start
+    spec.deploys[0].cap_sel = abi.CAP_OD
+    spec.pools[0].profile[abi.PROFILE_OFFPEAK].policy = abi.WHEN_EMPTY_OR_UNDERUTILIZED
+    n = 1100
+    sc = configs.hpa_scenarios(n, first_id=77)
+    load = po.gen_load(configs.trace_gen(4), spec.n_steps, 1, n, first_id=sc.first_id)
+    engine.lib.ccka_debug_lpw.argtypes = [C.c_void_p, C.c_int32]
+    assert engine.lib.ccka_debug_lpw(engine.ctx, lpw) == 0
+    try:
+        rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    finally:
+        engine.lib.ccka_debug_lpw(engine.ctx, 0)
+    assert engine.last_engine()[0] == 2
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    if max_nodes > 2:
+        assert ((tc["flags"] & 32) != 0).any()  # replacements happened
+    compare(rg, rc, tg, tc)
+
+
 def test_replacement_parity_multi_deployment(engine):
     spec = configs.config2_world(max_nodes=12)
     spec.replace = 1
