@@ -324,6 +324,34 @@ def test_d1_matches_general_kernel(engine):
     compare(r2, r1, t2, t1)
 
 
+def test_d1_replacement_large_catalog(engine):
+    """Replacement consolidation on the 800-type, 8-region catalog with
+    carbon weights: the single-deployment kernel's price-only offer table
+    (multi-chunk prefix scan) against the general kernel's per-lane offer
+    search and the oracle, bit for bit."""
+    spec = configs.config3_world(n_steps=720)
+    spec.replace = 1
+    spec.pdb_pct = -1
+    spec.deploys[0].cap_sel = abi.CAP_OD
+    spec.pools[0].profile[abi.PROFILE_OFFPEAK].policy = abi.WHEN_EMPTY_OR_UNDERUTILIZED
+    n = 1200
+    sc = configs.hpa_scenarios(n, 0, 8, 150, configs.CONFIG3_CARBON)
+    load = po.gen_load(configs.trace_gen(6), spec.n_steps, 1, n)
+    r2, t2 = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    engine.set_engine(1)
+    try:
+        engine.rollout(trajectory=True)
+        assert engine.last_engine()[0] == 1
+        r1, t1 = engine.results(), engine.trajectory()
+    finally:
+        engine.set_engine(0)
+    compare(r2, r1, t2, t1)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    assert ((tc["flags"] & 32) != 0).any()  # replacements happened
+    compare(r2, rc, t2, tc)
+
+
 @pytest.mark.parametrize("variant", ["drift", "drift_pdb_budget", "drift_delay0_bdef"])
 def test_d1_drift_matches_general_kernel(engine, variant):
     """The single-deployment kernel's drift (pre-spun replacements, takeovers,
