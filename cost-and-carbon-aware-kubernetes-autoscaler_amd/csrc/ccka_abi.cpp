@@ -248,8 +248,8 @@ static int d1_check_world(ccka_ctx* c) {
   c->d1_ready = false;
   const ccka_deployment& dp = w.deploy[0];
   if (w.n_deploy != 1 || dp.scaler != CCKA_SCALER_HPA) return CCKA_OK;
-  // replacement / multi-node consolidation run on the general kernel unless
-  // d1_prepare proves them inert for these scenarios (d1_disrupt_ok)
+  // pool limits run on the general kernel; drift, replacement and multi-node
+  // consolidation are checked per scenario set in d1_prepare (d1_disrupt_ok)
   for (int q = 0; q < w.n_pools; ++q)
     if (w.pools[q].limit_cpu_m >= 0 || w.pools[q].limit_mem_mi >= 0) return CCKA_OK;
   // one HPA decision per step over the 8-entry register rings
