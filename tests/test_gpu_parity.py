@@ -488,7 +488,7 @@ def test_keda_trigger_validation(engine):
 # single-node replacement consolidation (SEMANTICS 3.G2)
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("variant", ["spot_pool_only", "od_pool_weou", "drift_replace", "pdb50", "delay0",
-                                     "pool_limit"])
+                                     "pool_limit", "one_pool_budget50"])
 def test_replacement_parity_single_deployment(engine, variant):
     spec = configs.config2_world(n_steps=1440)
     spec.replace = 1
@@ -509,6 +509,10 @@ def test_replacement_parity_single_deployment(engine, variant):
     elif variant == "pool_limit":
         for p in spec.pools:
             p.limit_cpu_m = 12000
+    elif variant == "one_pool_budget50":  # the on-demand pool alone, half its nodes per step
+        spec.pools = [spec.pools[0]]
+        spec.pools[0].budget_pct = 50
+        spec.drift = 1
     load = po.gen_load(configs.trace_gen(3), spec.n_steps, 1, n, first_id=sc.first_id)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
     # replacement runs inside the single-deployment kernel (8 slots, <= 2 pools,
