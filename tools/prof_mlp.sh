@@ -5,7 +5,7 @@ out="$1"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p "$out"
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- \
-  python3 bench.py --config 5 --steps 5 --warmup 1 --no-cpu > "$out/trace.log" 2>&1 || exit $?
+  python3 bench.py --config 5 --steps 20 --warmup 3 --no-cpu > "$out/trace.log" 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS \
   SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS \
   -d "$out/pmc1" -o run --output-format csv -- python3 bench.py --config 5 --steps 1 --warmup 0 --no-cpu \
