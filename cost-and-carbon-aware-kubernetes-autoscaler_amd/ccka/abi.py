@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 STEP_SECONDS = 60
 MAX_TYPES = 1024
 MAX_ZONES = 4
@@ -118,6 +118,7 @@ class Totals(C.Structure):
     _fields_ = [("scenarios", C.c_int64), ("cost_uphmin", C.c_int64), ("slo_minutes", C.c_int64),
                 ("pending_pod_minutes", C.c_int64), ("node_min_spot", C.c_int64),
                 ("node_min_od", C.c_int64), ("launches", C.c_int64), ("deletions", C.c_int64),
+                ("energy_nwmin", C.c_int64), ("gco2_ug", C.c_int64),
                 ("energy_wmin", C.c_double), ("gco2", C.c_double)]
 
 
@@ -213,6 +214,8 @@ def load_engine(path: str | None = None):
         "ccka_last_kernel_ms": (C.c_int, [vp, C.POINTER(C.c_double)]),
         "ccka_get_results": (C.c_int, [vp, C.POINTER(Results)]),
         "ccka_get_trajectory": (C.c_int, [vp, C.POINTER(TrajRec), C.c_int64]),
+        "ccka_trajectory_layout": (C.c_int, [vp, C.POINTER(C.c_int32)]),
+        "ccka_get_trajectory_native": (C.c_int, [vp, C.POINTER(TrajRec), C.c_int64, C.POINTER(C.c_int32)]),
         "ccka_get_totals": (C.c_int, [vp, C.POINTER(Totals)]),
         "ccka_set_detail": (C.c_int, [vp, C.c_int32]),
         "ccka_policy_rollout": (C.c_int, [vp, C.c_int32, C.c_int32]),
@@ -241,8 +244,9 @@ EXPORTED = [
     "ccka_allreduce_totals", "ccka_comm_info", "ccka_device_info", "ccka_get_grid_stats", "ccka_pareto_frontier",
     "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
     "ccka_mlp_forward_async", "ccka_mlp_get_actions", "ccka_set_detail", "ccka_get_detail",
-    "ccka_policy_rollout", "ccka_get_policy_actions",
+    "ccka_policy_rollout", "ccka_get_policy_actions", "ccka_trajectory_layout", "ccka_get_trajectory_native",
 ]
+TRAJ_TN, TRAJ_NT = 0, 1  # device layouts of the trajectory records (ccka_trajectory_layout)
 
 
 def check_sizes(lib) -> None:

@@ -96,6 +96,17 @@ class Engine:
                                                a.size), "ccka_get_trajectory")
         return a
 
+    def trajectory_native(self):
+        """(records, layout): the device records without a transpose, shaped
+        [N][T] (abi.TRAJ_NT, the single-deployment engine) or [T][N]."""
+        lay = C.c_int32()
+        self._chk(self.lib.ccka_trajectory_layout(self.ctx, C.byref(lay)), "ccka_trajectory_layout")
+        shape = (self.n, self.T) if lay.value == abi.TRAJ_NT else (self.T, self.n)
+        a = np.zeros(shape, TRAJ_DTYPE)
+        self._chk(self.lib.ccka_get_trajectory_native(self.ctx, a.ctypes.data_as(C.POINTER(abi.TrajRec)), a.size,
+                                                      None), "ccka_get_trajectory_native")
+        return a, lay.value
+
     def totals(self) -> abi.Totals:
         t = abi.Totals()
         self._chk(self.lib.ccka_get_totals(self.ctx, C.byref(t)), "ccka_get_totals")

@@ -62,7 +62,7 @@ struct ccka_ctx {
   int64_t traj_count = 0;
   bool traj_valid = false;
   bool traj_nt = false;              // device records are [N][T] (single-deployment engine)
-  ccka_traj_rec* d_traj_t = nullptr;  // [T][N] copy for ccka_get_trajectory
+  ccka_traj_rec* d_traj_t = nullptr;  // [T][N] staging blocks for ccka_get_trajectory
   int64_t traj_t_count = 0;
   void* d_parts = nullptr;
   ccka_totals* d_totals = nullptr;
@@ -142,6 +142,9 @@ struct ccka_ctx {
   DetailDev* d_detail = nullptr;
   int64_t detail_count = 0;
 };
+
+// staging records of ccka_get_trajectory's [N][T] -> [T][N] transpose (64 MiB)
+constexpr int64_t kTrajStageRecs = int64_t(4) << 20;
 
 static int fail(ccka_ctx* c, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
 static int fail(ccka_ctx* c, int code, const char* fmt, ...) {
@@ -1221,19 +1224,50 @@ int ccka_get_trajectory(ccka_ctx* c, ccka_traj_rec* out, int64_t count) {
   if (!c->traj_valid) return fail(c, CCKA_ESTATE, "last rollout had no trajectory");
   if (count != c->traj_count) return fail(c, CCKA_EINVAL, "trajectory count mismatch");
   (void)hipSetDevice(c->device);
-  const ccka_traj_rec* src = c->d_traj;
-  if (c->traj_nt) {  // the single-deployment engine writes [N][T]: transpose on the device
-    if (c->traj_t_count != count) {
-      dfree(c->d_traj_t);
-      c->traj_t_count = 0;
-      if (hipMalloc((void**)&c->d_traj_t, (size_t)count * sizeof(ccka_traj_rec)) != hipSuccess)
-        return fail(c, CCKA_ENOMEM, "trajectory transpose alloc");
-      c->traj_t_count = count;
-    }
-    HIPCHK(c, launch_traj_transpose(c->d_traj, c->d_traj_t, c->N, count / c->N, c->stream));
-    src = c->d_traj_t;
+  if (!c->traj_nt) {  // already [T][N]
+    HIPCHK(c, hipMemcpyAsync(out, c->d_traj, (size_t)count * sizeof(ccka_traj_rec), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return CCKA_OK;
   }
-  HIPCHK(c, hipMemcpyAsync(out, src, (size_t)count * sizeof(ccka_traj_rec), hipMemcpyDeviceToHost, c->stream));
+  // the single-deployment engine keeps [N][T] on the device: transpose tc
+  // steps at a time into a bounded staging buffer (>= one step of N records,
+  // else kTrajStageRecs) and copy each block of steps to its place in out
+  const int64_t N = c->N, T = count / N;
+  const int64_t cap = std::max<int64_t>(N, std::min<int64_t>(count, kTrajStageRecs));
+  if (c->traj_t_count < cap) {
+    dfree(c->d_traj_t);
+    c->traj_t_count = 0;
+    if (hipMalloc((void**)&c->d_traj_t, (size_t)cap * sizeof(ccka_traj_rec)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "trajectory staging alloc (%lld records)", (long long)cap);
+    c->traj_t_count = cap;
+  }
+  const int64_t tc = std::max<int64_t>(1, c->traj_t_count / N);
+  for (int64_t t0 = 0; t0 < T; t0 += tc) {
+    const int64_t n = std::min(tc, T - t0);
+    HIPCHK(c, launch_traj_transpose(c->d_traj, c->d_traj_t, N, T, t0, n, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out + t0 * N, c->d_traj_t, (size_t)(n * N) * sizeof(ccka_traj_rec),
+                             hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_trajectory_layout(ccka_ctx* c, int32_t* layout) {
+  if (!c || !layout) return CCKA_EINVAL;
+  if (!c->traj_valid) return fail(c, CCKA_ESTATE, "last rollout had no trajectory");
+  *layout = c->traj_nt ? CCKA_TRAJ_NT : CCKA_TRAJ_TN;
+  return CCKA_OK;
+}
+
+int ccka_get_trajectory_native(ccka_ctx* c, ccka_traj_rec* out, int64_t count, int32_t* layout) {
+  if (!c || !out) return CCKA_EINVAL;
+  if (!c->traj_valid) return fail(c, CCKA_ESTATE, "last rollout had no trajectory");
+  if (count != c->traj_count) return fail(c, CCKA_EINVAL, "trajectory count mismatch");
+  (void)hipSetDevice(c->device);
+  if (layout) *layout = c->traj_nt ? CCKA_TRAJ_NT : CCKA_TRAJ_TN;
+  HIPCHK(c, hipMemcpyAsync(out, c->d_traj, (size_t)count * sizeof(ccka_traj_rec), hipMemcpyDeviceToHost,
+                           c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return CCKA_OK;
 }
@@ -1283,16 +1317,15 @@ int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
   if (!c->d_totals && hipMalloc((void**)&c->d_totals, sizeof(ccka_totals)) != hipSuccess)
     return fail(c, CCKA_ENOMEM, "totals alloc");
   HIPCHK(c, hipMemcpyAsync(c->d_totals, io, sizeof(ccka_totals), hipMemcpyHostToDevice, c->stream));
-  // 8 int64 fields then 2 doubles: one grouped pair of in-place all-reduces
-  ncclGroupStart();
-  ncclResult_t r1 = ncclAllReduce(c->d_totals, c->d_totals, 8, ncclInt64, ncclSum, c->comm, c->stream);
-  ncclResult_t r2 = ncclAllReduce(&c->d_totals->energy_wmin, &c->d_totals->energy_wmin, 2, ncclFloat64,
-                                  ncclSum, c->comm, c->stream);
-  ncclResult_t r3 = ncclGroupEnd();
-  if (r1 != ncclSuccess || r2 != ncclSuccess || r3 != ncclSuccess)
-    return fail(c, CCKA_ERCCL, "ncclAllReduce failed");
+  // the int64 block in one in-place all-reduce (exact, order-independent);
+  // the doubles are re-derived from it, so every rank count gives the same bits
+  const ncclResult_t r = ncclAllReduce(c->d_totals, c->d_totals, CCKA_TOTALS_INT64, ncclInt64, ncclSum,
+                                       c->comm, c->stream);
+  if (r != ncclSuccess) return fail(c, CCKA_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
   HIPCHK(c, hipMemcpyAsync(io, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  io->energy_wmin = (double)io->energy_nwmin * 1e-9;
+  io->gco2 = (double)io->gco2_ug * 1e-6;
   return CCKA_OK;
 }
 

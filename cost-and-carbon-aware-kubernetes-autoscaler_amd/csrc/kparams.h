@@ -93,7 +93,7 @@ struct TotParams {
   int64_t N;
 };
 
-constexpr int kPartBytes = 8 * 8 + 2 * 8;
+constexpr int kPartBytes = 10 * 8;
 
 // kernel instantiation chosen for (D, max_nodes): DMAX x MAXN
 inline void kernel_dims(int D, int maxn, int* dmax, int* nmax) {
@@ -265,7 +265,9 @@ hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipS
 hipError_t launch_policy_act(const float* y, int16_t* target, double* cw, int16_t* rec_target, double* rec_cw,
                              int64_t n, hipStream_t s);
 hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s);
-// [N][T] (single-deployment engine, device side) -> [T][N] (ccka_traj_rec order of the ABI)
-hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, hipStream_t s);
+// [N][T] (single-deployment engine, device side) -> steps [t0, t0 + tc) of the
+// [T][N] order ccka_get_trajectory returns, into out[tc][N]
+hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, int64_t t0,
+                                 int64_t tc, hipStream_t s);
 
 }  // namespace ccka

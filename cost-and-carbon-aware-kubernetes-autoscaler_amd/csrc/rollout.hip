@@ -2084,8 +2084,7 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
 // Totals: fixed-order block partials, then one ordered final pass.
 // ---------------------------------------------------------------------------
 struct Part {
-  long long v[8];
-  double e, g;
+  long long v[10];  // ccka_totals' int64 block (energy and gCO2 in fixed point)
 };
 
 __global__ void __launch_bounds__(256) totals_partial(TotParams q) {
@@ -2093,9 +2092,7 @@ __global__ void __launch_bounds__(256) totals_partial(TotParams q) {
   const int tid = threadIdx.x;
   Part a;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) a.v[k] = 0;
-  a.e = 0.0;
-  a.g = 0.0;
+  for (int k = 0; k < 10; ++k) a.v[k] = 0;
   const int64_t chunk = (q.N + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(lo + chunk, q.N);
   for (int64_t i = lo + tid; i < hi; i += blockDim.x) {
@@ -2107,17 +2104,15 @@ __global__ void __launch_bounds__(256) totals_partial(TotParams q) {
     a.v[5] += q.nmin_od[i];
     a.v[6] += q.launches[i];
     a.v[7] += q.deletions[i];
-    a.e += q.energy[i];
-    a.g += q.gco2[i];
+    a.v[8] += __double2ll_rn(q.energy[i] * 1e9);  // llrint, as ccka_oracle_totals
+    a.v[9] += __double2ll_rn(q.gco2[i] * 1e6);
   }
   sp[tid] = a;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (tid < s) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) sp[tid].v[k] += sp[tid + s].v[k];
-      sp[tid].e += sp[tid + s].e;
-      sp[tid].g += sp[tid + s].g;
+      for (int k = 0; k < 10; ++k) sp[tid].v[k] += sp[tid + s].v[k];
     }
     __syncthreads();
   }
@@ -2127,14 +2122,9 @@ __global__ void __launch_bounds__(256) totals_partial(TotParams q) {
 __global__ void totals_final(TotParams q, int nparts) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Part a;
-  for (int k = 0; k < 8; ++k) a.v[k] = 0;
-  a.e = 0.0;
-  a.g = 0.0;
-  for (int b = 0; b < nparts; ++b) {
-    for (int k = 0; k < 8; ++k) a.v[k] += q.parts[b].v[k];
-    a.e += q.parts[b].e;
-    a.g += q.parts[b].g;
-  }
+  for (int k = 0; k < 10; ++k) a.v[k] = 0;
+  for (int b = 0; b < nparts; ++b)
+    for (int k = 0; k < 10; ++k) a.v[k] += q.parts[b].v[k];
   ccka_totals* o = q.out;
   o->scenarios = a.v[0];
   o->cost_uphmin = a.v[1];
@@ -2144,8 +2134,10 @@ __global__ void totals_final(TotParams q, int nparts) {
   o->node_min_od = a.v[5];
   o->launches = a.v[6];
   o->deletions = a.v[7];
-  o->energy_wmin = a.e;
-  o->gco2 = a.g;
+  o->energy_nwmin = a.v[8];
+  o->gco2_ug = a.v[9];
+  o->energy_wmin = (double)a.v[8] * 1e-9;
+  o->gco2 = (double)a.v[9] * 1e-6;
 }
 
 // ---------------------------------------------------------------------------

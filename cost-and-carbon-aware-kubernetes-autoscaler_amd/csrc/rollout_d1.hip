@@ -321,22 +321,31 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_VMN_V 12
 #endif
 #ifndef D1_LEAN_V
-#define D1_LEAN_V 1
+#define D1_LEAN_V 2
 #endif
 #ifndef D1_S_V
 #define D1_S_V 4
+#endif
+// LEAN 2: 1 = a proposal below cur held by the down window is a quiet step
+// (its record is rebuilt at the next event), 0 = such a step is an event, so
+// every quiet record is cur and the rebuild is a fill
+#ifndef D1_HELD_V
+#define D1_HELD_V 0
 #endif
 constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
 constexpr int D1_K = D1_K_V;      // event cadence (iterations)
 constexpr int D1_VMN = D1_VMN_V;  // rows in flight (vmcnt bound; <= 63)
 constexpr int D1_S = D1_S_V;      // quiet steps per iteration and lane
-static_assert(D1_VMN + 8 * D1_S <= D1_RB, "ring too small for the DMA lead");
+// rows kept behind the slowest lane: the LEAN 2 event step rebuilds the
+// down-window records of its quiet steps from them (window <= CCKA_HIST steps)
+constexpr int D1_BACK = D1_LEAN_V == 2 ? CCKA_HIST : 0;
+// the initial fill (D1_VMN + 4 D1_S rows) plus the rows kept behind must fit,
+// and the lanes must be able to spread over a few iterations' worth of rows
+static_assert(D1_VMN + 4 * D1_S + D1_BACK <= D1_RB && D1_RB - D1_S - D1_BACK - D1_VMN >= 2 * D1_S,
+              "ring too small for the DMA lead");
 constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
 
-// streaming hint on the trace rows and trajectory records (build variants)
-#ifndef D1_NT_V
-#define D1_NT_V 0
-#endif
+// streaming hint on the trace rows (build variant)
 #ifndef D1_NTL_V
 #define D1_NTL_V 0
 #endif
@@ -345,14 +354,15 @@ constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
 #else
 #define D1_NTL ""
 #endif
-__device__ __forceinline__ void d1_store_rec(GLOBAL_AS int4* p, const int4& v) {
-#if D1_NT_V
+// Trajectory records go through a buffer resource over the wave's [lanes][T]
+// record block: the hardware drops a store whose offset lies past num_records,
+// so an out-of-range offset masks a lane's store without an exec-mask branch,
+// and num_records = 0 turns every store off when no trajectory is kept.
+constexpr int D1_NOSTORE = 0x7FFFFFF0;
+__device__ __forceinline__ void d1_store_rec(__amdgpu_buffer_rsrc_t r, int voff, const int4& v) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   const i32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, (GLOBAL_AS i32x4*)p);
-#else
-  *(int4*)p = v;
-#endif
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, 0);
 }
 
 __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row) {
@@ -547,6 +557,22 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   bool q_atmax = false, q_pend = false;  // cur >= maxReplicas, pending pods
   int q_umax = -1;  // largest usage the quiet step evaluates exactly (-1: every step is an event)
   const int wl = __popc(dnmask);  // down window: the last wl records
+  // LEAN 2 quiet step (default behavior): the HPA outcome of a quiet step is a
+  // pair of integer compares on the step's usage. Between two event steps the
+  // replica count, the ready pods and the node set are constant, so the
+  // proposal is a monotone step function of usage and the step is quiet iff
+  //   usage < q_ulim            (proposal <= cur, or any proposal at maxReplicas;
+  //                              and usage < 2^20, the exact range of upp below)
+  //   usage >= q_pge || t <= q_hold   (proposal >= cur, or a record >= cur is
+  //                              still inside the down-stabilisation window)
+  // The records themselves are not pushed: the next event step rebuilds the
+  // ones inside the window from the trace rows still in the LDS ring. The
+  // step's dynamic energy Ssum * upp is accumulated as sum(upp) and charged at
+  // the next flush; SLO is usage >= q_slo.
+  int q_ulim = 0, q_pge = 0, q_slo = 0, q_usat = 0, q_w0 = 0, q_w1 = 0, q_pendv = 0, q_nodes = 0;
+  float q_hbp = 0.f;   // 0.5 / ready pods (upp = (usage + 0.5) / ready pods, truncated)
+  uint32_t usum = 0;   // sum of upp over the quiet steps since the last flush
+  bool q_met = false;  // the HPA has a metric (records are proposals, else invalid)
 
   auto refresh_J = [&](int rh) {
 #pragma unroll
@@ -697,6 +723,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     const int n = upto - tq;
     cost += (burn + base_price) * (long long)n;
     e_hour += (base_nw + Isum) * (long long)n;
+    if constexpr (BDEF && D1_LEAN_V == 2) {  // dynamic energy of the quiet steps (exact integers)
+      e_hour += (long long)(Ssum * (unsigned long long)usum);
+      usum = 0;
+    }
     pend_min += (replicas - rpods) * n;
     nmin_spot += nsp * n;
     nmin_od += nod * n;
@@ -728,7 +758,17 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // trajectory records scenario-major on the device ([N][T]: a lane's records
   // are contiguous, so its consecutive steps fill whole lines however far the
   // lanes drift apart); ccka_get_trajectory returns them [T][N]
-  GLOBAL_AS int4* tp = traj + i * (int64_t)T;  // this lane's record of step t
+  const int64_t w0 = [&] {  // the wave's first scenario (wave-uniform)
+    const int64_t x = wv * p.lpw;
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(x & 0xffffffffLL));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  }();
+  const int wlanes = (int)min((int64_t)p.lpw, p.N - w0);
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
+      traj ? (void*)(reinterpret_cast<int4*>(p.traj) + w0 * T) : (void*)p.load, 0, traj ? wlanes * T * 16 : 0,
+      0x00020000);
+  const int lb = lane * T * 16;  // this lane's record of step t at byte lb + 16 t
 
   for (int it = 0;; ++it) {
     const bool live = t < T;
@@ -756,6 +796,53 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       if (ev) {
         stall = false;
         L = ring[(t & (D1_RB - 1)) * WAVE + lane];
+        if constexpr (BDEF && D1_LEAN_V == 2) {
+          // the down-window records of the quiet steps [tq, t), oldest first,
+          // from their trace rows (the ring keeps >= 8 rows behind every lane)
+          // and the state they ran with. A record >= cur is stored as cur: the
+          // default behavior only ever compares it with a proposal and with cur
+          // (<= maxReplicas), so its excess over cur never changes a decision.
+          const int kq = min(t - tq, wl);
+          if constexpr (!D1_HELD_V) {
+            // every quiet record is cur (or invalid without a metric)
+            const int rv = q_met ? min(replicas, D1_REC_SAT) : (int)0x8000;
+            const uint32_t rr = ((uint32_t)rv & 0xFFFFu) * 0x10001u;
+            if (kq >= wl) {  // the whole window is quiet steps (entries >= wl are never read)
+#pragma unroll
+              for (int w = 0; w < 4; ++w) hdn[w] = rr;
+            } else {
+#pragma unroll
+              for (int j = 1; j < CCKA_HIST; ++j)
+                if (j <= kq) ring_push(hdn, rv);
+            }
+          } else
+          if (kq > 0) {
+            const int cur16 = min(replicas, D1_REC_SAT);
+            const int dreq = rpods * req;
+            const float rbd = __builtin_amdgcn_rcpf((float)dreq);
+#pragma unroll
+            for (int j = CCKA_HIST; j >= 1; --j) {
+              if (j <= kq) {
+                const int us = min(ring[((t - j) & (D1_RB - 1)) * WAVE + lane], q_rcap);
+                int rv = q_met ? cur16 : (int)0x8000;
+                if (q_met && us < q_pge) {
+                  // held below cur: util < ulo <= target, so no unready rule and the
+                  // proposal is ceil(util * ready / target) (binary64 at an exact
+                  // multiple, as the spec writes it); us < 2^20 and util < 2^15
+                  // keep both f32 quotients exact after one correction
+                  bool sl = false;
+                  const int util = fdiv_nb(us * 100, dreq, rbd, sl);
+                  const int x = (int)__umul24((uint32_t)util, (uint32_t)rpods);
+                  const int q = fdiv_nb(x, target, rtarget, sl);
+                  int c = q + (x == q * target ? 0 : 1);
+                  if (__builtin_expect(x == q * target, 0)) c = (int)ceil(((double)util / (double)target) * (double)rpods);
+                  rv = min(c, D1_REC_SAT);
+                }
+                ring_push(hdn, rv);
+              }
+            }
+          }
+        }
         flush(t);
         minute = (sm0 + t) % 1440;
         const int h = minute / 60;
@@ -1395,7 +1482,69 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                         (step_last_type & 0xFFFF) | (int)(flags << 16));
 
         // ---- caches of the quiet steps that follow ----
-        {
+        if constexpr (BDEF && D1_LEAN_V == 2) {
+          constexpr int UQ = 1 << 20;  // quiet usages: [0, 2^20)
+          // smallest usage with floor(100 * usage / d) >= u (u >= 0), capped at UQ
+          auto umin = [](int u, uint32_t d) -> int {
+            const unsigned long long a = (unsigned long long)(uint32_t)u * d;
+            return a > 100ull * UQ ? UQ : min((int)(((uint32_t)a + 99u) / 100u), UQ);
+          };
+          const bool hpa_path = !(replicas == 0 && minr != 0);
+          const bool met = replicas <= mx && replicas >= minr && rpods > 0 && hpa_path;
+          const int dnm = replicas > mx ? mx : (replicas < minr && hpa_path ? minr : replicas);
+          const bool pend = replicas > rpods;
+          q_met = met;
+          q_rcap = limit > 0 ? (int)__umul24((uint32_t)rpods, (uint32_t)limit) : 0x7fffffff;
+          const uint32_t dreq = (uint32_t)rpods * (uint32_t)req;  // < 2^31
+          int ulim = 0, pge = UQ, slo_thr = pend ? 0 : UQ;
+          if (met) {
+            // util = floor(100 usage / dreq); keep: ulo <= util <= uhi
+            int uge = ulo;  // proposal >= cur from this util on
+            int lim;        // proposal <= cur below this usage
+            if (pend) {
+              // unready pods (cur > ready): util <= target proposes ceil(util*ready/target)
+              // < cur outside the band; util > target counts every replica (nu =
+              // floor(100 usage / (cur*req))): keep iff nu <= uhi, else above cur
+              lim = max(umin(target + 1, dreq), umin(uhi + 1, (uint32_t)replicas * (uint32_t)req));
+            } else {
+              // below the band the proposal ceil(util*cur/target) reaches cur from
+              // us = floor((cur-1)*target/cur) + 1 on (binary64 at an exact multiple
+              // may round one below that up to cur as well)
+              bool sl = false;
+              const int cq = fdiv_nb(target + replicas - 1, replicas, __builtin_amdgcn_rcpf((float)replicas), sl);
+              int us = target - cq + 1;
+              const int um = us - 1;  // < target, so um * cur < 2^30
+              if (um >= 0) {
+                const int xm = um * replicas;
+                const int qm = fdiv_nb(xm, target, rtarget, sl);
+                if (__builtin_expect(xm == qm * target, 0) &&
+                    (int)ceil(((double)um / (double)target) * (double)replicas) >= replicas)
+                  us = um;
+              }
+              uge = min(uge, max(us, 0));
+              lim = umin(uhi + 1, dreq);
+            }
+            pge = umin(uge, dreq);
+            ulim = replicas >= mx ? UQ : lim;
+            if (!pend) slo_thr = umin(max(slo_util + 1, 0), dreq);
+          } else if (dnm == replicas) {
+            ulim = UQ;  // no metric, replicas in range: every step keeps them
+          }
+          q_ulim = ulim;
+          q_pge = pge;
+          q_slo = slo_thr;
+          // upp = floor(usage / ready) = trunc((usage + 0.5) / ready) in binary32 for
+          // usage < 2^20 (the quotient stays 0.5/ready clear of an integer; the
+          // correctly rounded reciprocal and the single fma rounding are far inside that)
+          q_rbp = rpods > 0 ? 1.0f / (float)rpods : 0.f;
+          q_hbp = 0.5f * q_rbp;
+          // no node saturates while upp <= q_usat (pods*upp < alloc on every node)
+          q_usat = Rmax > 0.f ? (int)fminf(0.9999f * __builtin_amdgcn_rcpf(Rmax), 1073741824.0f) - 1 : 0x7fffffff;
+          q_pendv = replicas - rpods;
+          q_nodes = (nsp & 0xFFFF) | nod << 16;
+          q_w0 = 0xFFFF | (int)((q_peak ? 1u : 0u) << 16);
+          q_w1 = q_w0 | (8 << 16);
+        } else {
           q_rbd = __builtin_amdgcn_rcpf((float)(rpods * req));
           q_rbc = __builtin_amdgcn_rcpf((float)(replicas * req));
           // (rpods, replicas <= 32767 and req, limit <= 65535: exact 24-bit products)
@@ -1411,15 +1560,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           q_unr = replicas > rpods;
           q_atmax = replicas >= mx;
           q_pend = replicas > rpods;
-          if constexpr (BDEF) {  // newest history record >= the new replica count
-            int hit = -0x40000000;
-#pragma unroll
-            for (int k = CCKA_HIST - 1; k >= 0; --k) {
-              const int e = (int)(short)(hdn[k >> 1] >> (16 * (k & 1)));
-              hit = e >= replicas ? t - k : hit;
-            }
-            q_hold = replicas <= minr ? 0x3fffffff : hit + wl;
-          }
           // Exactness range of the quiet step's arithmetic: usage < 2^20 (f32
           // exact), util < 2^16 (usage*100 < 2^16*ready*req), and proposal
           // estimates u*base/target < 2^20 for u < 2^16 (base < 16*target), so
@@ -1434,6 +1574,17 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             const bool ok = q_mode < 2 && base_max < 16 * target && (!q_unr || q_dcur < (1 << 24));
             q_umax = !ok ? -1 : (q_mode == 1 ? 0x7fffffff : ucap);
           }
+        }
+        if constexpr (BDEF) {  // newest history record >= the new replica count
+          int hit = -0x40000000;
+#pragma unroll
+          for (int k = CCKA_HIST - 1; k >= 0; --k) {
+            const int e = (int)(short)(hdn[k >> 1] >> (16 * (k & 1)));
+            hit = e >= replicas ? t - k : hit;
+          }
+          q_hold = replicas <= minr ? 0x3fffffff : hit + wl;
+          // LEAN 2 without a metric: no records, nothing to hold
+          if (D1_LEAN_V == 2 && !q_met) q_hold = 0x3fffffff;
         }
         // first step that needs the event path again: a node becomes ready,
         // an hour or peak-window boundary, a slot becomes a consolidation
@@ -1461,8 +1612,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         }
       }
       if (ev) {
-        if (traj) d1_store_rec(tp, rec);
-        ++tp;
+        d1_store_rec(trs, lb + t * 16, rec);
         ++t;
       }
       pf_ok = pf_ok && !ev;
@@ -1472,7 +1622,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     // what they overwrite; issued after the event steps, whose own loads
     // wait for every older vector-memory operation ----
     if (tf < T) {
-      if (__ballot(t < T && t < tf + D1_S - D1_RB) == 0) {
+      if (__ballot(t < T && t < tf + D1_S - D1_RB + D1_BACK) == 0) {
         const int n1 = min(T, tf + D1_S);
         for (; tf < n1; ++tf)
           d1_dma_row(lpf, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4)), lpf += lsl;
@@ -1490,13 +1640,36 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 
     D1_STAMP(8);
     // ---- quiet steps: up to D1_S per iteration and lane ----
+    const int tlim = min(T, t_rdy);
 #pragma unroll
     for (int sub = 0; sub < D1_S; ++sub) {
+    if constexpr (BDEF && D1_LEAN_V == 2) {
+        const int L = Lpf[sub];
+        // two usage compares decide the HPA (see q_ulim / q_pge); the rest is
+        // accounting, the SLO test and the trajectory record, all predicated
+        // on `go` (no branch but the rare saturation one)
+        const int usage = min(L, q_rcap);
+        const bool ge = usage >= q_pge;
+        const bool ok = (t < nxt) & ((uint32_t)usage < (uint32_t)q_ulim) & (ge | (D1_HELD_V && t <= q_hold));
+        const bool can = !stall & (t < tlim);
+        const bool go = ok & can;
+        stall = stall | (can & !ok);
+        if constexpr (D1_HELD_V) q_hold = (go & ge) ? max(q_hold, t + wl) : q_hold;
+        const int upp = (int)fmaf((float)usage, q_rbp, q_hbp);
+        if (__builtin_expect(go & (upp > q_usat), 0))  // a node may saturate: exact per-node sum instead
+          e_hour += dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+        usum += go ? (uint32_t)upp : 0u;
+        const bool slo_b = usage >= q_slo;
+        slo += (go & slo_b) ? 1 : 0;
+        d1_store_rec(trs, go ? lb + t * 16 : D1_NOSTORE, make_int4(replicas, q_pendv, q_nodes, slo_b ? q_w1 : q_w0));
+        t += go ? 1 : 0;
+        adv = adv | go;
+    } else
     if (t < T && !stall && t < t_rdy) {
       // a lane still stepping in sub-step `sub` has advanced in every earlier one
       const int L = Lpf[sub];
       int4 rec;
-      if constexpr (BDEF && D1_LEAN_V) {
+      if constexpr (BDEF && D1_LEAN_V == 1) {
         // Upstream default behavior, decided without the general path:
         // keep (util inside the tolerance band) leaves the replicas; a
         // proposal above cur changes nothing at maxReplicas; one below cur
@@ -1557,8 +1730,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             rec = make_int4(cur, cur - rpods, (nsp & 0xFFFF) | nod << 16,
                             0xFFFF | (int)((q_peak ? 1u : 0u) << 16) | (slo_b ? (8 << 16) : 0));
             adv = true;
-            if (traj) d1_store_rec(tp, rec);
-            ++tp;
+            d1_store_rec(trs, lb + t * 16, rec);
             ++t;
           }
         }
@@ -1576,8 +1748,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           const uint32_t flags = (q_peak ? 1u : 0u) | (slo_b ? 8u : 0u);
           rec = make_int4(replicas, pending, (nsp & 0xFFFF) | nod << 16, 0xFFFF | (int)(flags << 16));
           adv = true;
-          if (traj) d1_store_rec(tp, rec);
-          ++tp;
+          d1_store_rec(trs, lb + t * 16, rec);
           ++t;
         }
       }
@@ -1619,30 +1790,35 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 }
 
 // [N][T] -> [T][N] trajectory records (ccka_get_trajectory after the
-// single-deployment engine): 32 x 32 tiles through LDS, 16-byte elements,
-// both sides coalesced.
+// single-deployment engine), steps [t0, t0 + tc) at a time into a bounded
+// staging buffer: 32 x 32 tiles through LDS, 16-byte elements, both sides
+// coalesced; the tiles are numbered on grid.x alone (no grid.y limit on N).
 __global__ void __launch_bounds__(256) traj_transpose_kernel(const int4* __restrict__ in, int4* __restrict__ out,
-                                                             int64_t N, int64_t T) {
+                                                             int64_t N, int64_t T, int64_t t0, int64_t tc) {
   __shared__ int4 tile[32][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  const int64_t t0 = (int64_t)blockIdx.x * 32, n0 = (int64_t)blockIdx.y * 32;
+  const int64_t ntn = (N + 31) / 32;
+  const int64_t tb = (int64_t)blockIdx.x / ntn * 32, n0 = (int64_t)blockIdx.x % ntn * 32;
 #pragma unroll
   for (int k = 0; k < 32; k += 8) {
-    const int64_t n = n0 + ty + k, t = t0 + tx;
-    if (n < N && t < T) tile[ty + k][tx] = in[n * T + t];
+    const int64_t n = n0 + ty + k, t = tb + tx;
+    if (n < N && t < tc) tile[ty + k][tx] = in[n * T + t0 + t];
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 32; k += 8) {
-    const int64_t t = t0 + ty + k, n = n0 + tx;
-    if (n < N && t < T) out[t * N + n] = tile[tx][ty + k];
+    const int64_t t = tb + ty + k, n = n0 + tx;
+    if (n < N && t < tc) out[t * N + n] = tile[tx][ty + k];
   }
 }
 
-hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, hipStream_t s) {
-  const dim3 grid((unsigned)((T + 31) / 32), (unsigned)((N + 31) / 32));
-  hipLaunchKernelGGL(traj_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const int4*>(in),
-                     reinterpret_cast<int4*>(out), N, T);
+hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, int64_t t0,
+                                 int64_t tc, hipStream_t s) {
+  const int64_t blocks = (N + 31) / 32 * ((tc + 31) / 32);
+  if (blocks <= 0) return hipSuccess;
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(traj_transpose_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                     reinterpret_cast<const int4*>(in), reinterpret_cast<int4*>(out), N, T, t0, tc);
   return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CCKA_ABI_VERSION 3
+#define CCKA_ABI_VERSION 4
 
 #define CCKA_STEP_SECONDS 60
 #define CCKA_MAX_TYPES 1024
@@ -249,7 +249,12 @@ typedef struct ccka_detail {
   double base_gco2;
 } ccka_detail;
 
-/* Trajectory record, one per (step, scenario), layout [T][N]. 16 bytes. */
+/* Trajectory record, one per (step, scenario). 16 bytes. ccka_get_trajectory
+ * returns them step-major [T][N]; on the device they stay in the layout the
+ * engine wrote (ccka_trajectory_layout): the single-deployment engine writes
+ * scenario-major [N][T] (each scenario's horizon contiguous), the general
+ * engine step-major [T][N]. */
+enum { CCKA_TRAJ_TN = 0, CCKA_TRAJ_NT = 1 };
 typedef struct ccka_traj_rec {
   int32_t replicas;
   int32_t pending;
@@ -259,8 +264,12 @@ typedef struct ccka_traj_rec {
   uint16_t flags;
 } ccka_traj_rec;
 
-/* Whole-batch totals (packed for one all-reduce). Integer fields are exact and
- * order-independent; doubles are summed in a fixed tree order per device. */
+/* Whole-batch totals (packed for one all-reduce). Every summed field is an
+ * int64, so sums are exact and independent of the summation order, the device
+ * tree and the rank count: energy and gCO2 are summed in fixed point, each
+ * scenario's value rounded once (llrint: to nearest, ties to even). The two
+ * doubles are derived from them after every sum (ccka_get_totals,
+ * ccka_allreduce_totals), so they too are bit-identical at any rank count. */
 typedef struct ccka_totals {
   int64_t scenarios;
   int64_t cost_uphmin;
@@ -270,9 +279,12 @@ typedef struct ccka_totals {
   int64_t node_min_od;
   int64_t launches;
   int64_t deletions;
-  double energy_wmin;
-  double gco2;
+  int64_t energy_nwmin;         /* sum of llrint(energy_wmin[i] * 1e9): nanowatt-minutes */
+  int64_t gco2_ug;              /* sum of llrint(gco2[i] * 1e6): micrograms              */
+  double energy_wmin;           /* energy_nwmin * 1e-9 */
+  double gco2;                  /* gco2_ug * 1e-6      */
 } ccka_totals;
+#define CCKA_TOTALS_INT64 10    /* leading int64 fields: the all-reduced block */
 
 /* Per-grid sums of a policy sweep (BASELINE config 4): grid g = the scenarios
  * with global ids [g*grid_size, (g+1)*grid_size). 48 bytes. */
@@ -321,9 +333,12 @@ int ccka_gen_load(ccka_ctx* ctx, const ccka_trace_gen* gen);
 int ccka_get_load(ccka_ctx* ctx, int32_t* load, int64_t count);
 
 /* ---- rollout --------------------------------------------------------- */
-/* Run the whole horizon for every scenario. trajectory != 0 also writes
- * the [T][N] trajectory records on the device. Results stay on the device
- * until ccka_get_results / ccka_get_trajectory / ccka_get_totals. */
+/* Run the whole horizon for every scenario. trajectory != 0 also writes one
+ * trajectory record per (step, scenario) on the device, in the engine's own
+ * layout (ccka_trajectory_layout: [N][T] from the single-deployment engine,
+ * whose kernel time ccka_last_kernel_ms reports with those writes included;
+ * [T][N] from the general engine). Results stay on the device until
+ * ccka_get_results / ccka_get_trajectory / ccka_get_totals. */
 int ccka_rollout(ccka_ctx* ctx, int32_t trajectory);
 int ccka_rollout_async(ccka_ctx* ctx, int32_t trajectory);
 int ccka_sync(ccka_ctx* ctx);
@@ -331,7 +346,15 @@ int ccka_sync(ccka_ctx* ctx);
  * stream (milliseconds). */
 int ccka_last_kernel_ms(ccka_ctx* ctx, double* ms);
 int ccka_get_results(ccka_ctx* ctx, ccka_results* out);
+/* The records in [T][N] order (count = T*N). From an [N][T] device layout the
+ * engine transposes blocks of steps on the device through a bounded staging
+ * buffer (max(N, 4 Mi) records) and copies each block into place. */
 int ccka_get_trajectory(ccka_ctx* ctx, ccka_traj_rec* out, int64_t count);
+/* Device layout of the last rollout's records (CCKA_TRAJ_TN / CCKA_TRAJ_NT). */
+int ccka_trajectory_layout(ccka_ctx* ctx, int32_t* layout);
+/* The records exactly as the device holds them (no transpose); *layout (nullable)
+ * receives CCKA_TRAJ_TN / CCKA_TRAJ_NT. */
+int ccka_get_trajectory_native(ccka_ctx* ctx, ccka_traj_rec* out, int64_t count, int32_t* layout);
 int ccka_get_totals(ccka_ctx* ctx, ccka_totals* out);
 /* on != 0: later rollouts also record the per-scenario ccka_detail (the
  * summary path: the run takes the general kernel; results are unchanged). */
@@ -387,7 +410,9 @@ int ccka_get_policy_actions(ccka_ctx* ctx, int16_t* target, double* cw, int64_t 
 /* Fill a 128-byte RCCL unique id (rank 0 only; distribute it out of band). */
 int ccka_comm_unique_id(uint8_t* id128);
 int ccka_comm_init(ccka_ctx* ctx, const uint8_t* id128, int32_t nranks, int32_t rank);
-/* In-place sum of the packed totals across ranks. */
+/* In-place sum of the packed totals across ranks: one RCCL all-reduce of the
+ * CCKA_TOTALS_INT64 int64 fields, then energy_wmin / gco2 re-derived from
+ * them (bit-identical at any rank count). */
 int ccka_allreduce_totals(ccka_ctx* ctx, ccka_totals* inout);
 /* Rank count and this context's rank as the RCCL communicator reports them
  * (ncclCommCount / ncclCommUserRank); CCKA_ESTATE without ccka_comm_init. */

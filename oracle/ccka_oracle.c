@@ -1403,7 +1403,9 @@ void ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* o) {
     o->node_min_od += r->node_min_od[i];
     o->launches += r->launches[i];
     o->deletions += r->deletions[i];
-    o->energy_wmin += r->energy_wmin[i];
-    o->gco2 += r->gco2[i];
+    o->energy_nwmin += llrint(r->energy_wmin[i] * 1e9);  /* fixed point, as the device totals */
+    o->gco2_ug += llrint(r->gco2[i] * 1e6);
   }
+  o->energy_wmin = (double)o->energy_nwmin * 1e-9;
+  o->gco2 = (double)o->gco2_ug * 1e-6;
 }
