@@ -296,8 +296,9 @@ def main():
         if cfg == 4:
             out["pareto_frontier_grids"] = frontier[-1] if frontier else None
         if rank == 0:
-            cbw = copy_bandwidth()
+            cbw = copy_bandwidth(eng)
             out["roofline"]["copy_gbs"] = cbw
+            out["roofline"]["copy_kernel"] = "copy16_kernel: 2 GiB dwordx4 nontemporal streaming copy, median of 5"
             out["roofline"]["frac_of_copy"] = achieved / cbw
         if rank == 0 and world == 1 and not args.no_cpu:
             out["cpu_baseline"], out["parity"], out["parity_detail"] = cpu_baseline(
@@ -324,26 +325,17 @@ def measured_traffic(cfg, traj, n, T):
     return json.load(open(paths[-1])).get("traffic_bytes")
 
 
-def copy_bandwidth(nbytes=1 << 31, reps=5):
-    """Measured device copy rate (GB/s of read + write) of a plain 2 GiB
-    device-to-device copy on this GPU, the practical HBM ceiling the rollout's
-    achieved bytes are also compared against."""
-    import torch
-
-    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    b = torch.empty_like(a)
-    b.copy_(a)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize()
-    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del a, b
-    torch.cuda.empty_cache()
-    return gbs
+def copy_bandwidth(eng, nbytes=1 << 31, reps=5):
+    """Measured device copy ceiling (GB/s of read + write): libccka's
+    copy16_kernel, a 2 GiB streaming copy with 16 bytes per lane per access
+    (dwordx4), timed with HIP events on the engine stream; the practical HBM
+    ceiling the rollout's achieved bytes are also compared against (SURVEY.md
+    8(d))."""
+    gbs = C.c_double()
+    fn = eng.lib.ccka_debug_copy_gbs
+    fn.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.POINTER(C.c_double)]
+    eng._chk(fn(eng.ctx, nbytes, reps, C.byref(gbs)), "ccka_debug_copy_gbs")
+    return gbs.value
 
 
 def profiled_issue(cfg):

@@ -1638,6 +1638,43 @@ int ccka_mlp_get_actions(ccka_ctx* c, float* y, int64_t n) {
 
 // Internal profiling hook (not part of include/ccka.h): phase-ablation mask
 // for timing attribution only; results of an ablated run are meaningless.
+// Internal: the device copy ceiling, GB/s of read + write of a `bytes`-byte
+// dwordx4 streaming copy (launch_copy16), the median of `reps` launches timed
+// with HIP events on the engine's stream after one warm-up launch.
+int ccka_debug_copy_gbs(ccka_ctx* c, int64_t bytes, int32_t reps, double* gbs) {
+  if (!c || !gbs || bytes < (1 << 20) || reps < 1 || reps > 64) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  bytes &= ~(int64_t)4095;
+  void *a = nullptr, *b = nullptr;
+  if (hipMalloc(&a, (size_t)bytes) != hipSuccess || hipMalloc(&b, (size_t)bytes) != hipSuccess) {
+    if (a) (void)hipFree(a);
+    return fail(c, CCKA_ENOMEM, "copy probe alloc (2 x %lld bytes)", (long long)bytes);
+  }
+  int rc = CCKA_OK;
+  std::vector<float> ms((size_t)reps);
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // own events: ccka_last_kernel_ms keeps the rollout's
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    rc = fail(c, CCKA_EHIP, "copy probe events");
+  if (rc == CCKA_OK && (hipMemsetAsync(a, 1, (size_t)bytes, c->stream) != hipSuccess ||
+      launch_copy16(a, b, bytes, c->cus, c->stream) != hipSuccess))
+    rc = fail(c, CCKA_EHIP, "copy probe warm-up");
+  for (int k = 0; k < reps && rc == CCKA_OK; ++k) {
+    if (hipEventRecord(e0, c->stream) != hipSuccess || launch_copy16(a, b, bytes, c->cus, c->stream) != hipSuccess ||
+        hipEventRecord(e1, c->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms[(size_t)k], e0, e1) != hipSuccess)
+      rc = fail(c, CCKA_EHIP, "copy probe launch %d", k);
+  }
+  (void)hipStreamSynchronize(c->stream);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  if (rc != CCKA_OK) return rc;
+  std::sort(ms.begin(), ms.end());
+  *gbs = 2.0 * (double)bytes / ((double)ms[(size_t)reps / 2] * 1e-3) / 1e9;
+  return CCKA_OK;
+}
+
 int ccka_debug_ablate(ccka_ctx* c, int32_t mask) {
   if (!c) return CCKA_EINVAL;
   c->kp.ablate = mask;

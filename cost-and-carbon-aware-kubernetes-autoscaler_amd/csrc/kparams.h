@@ -236,6 +236,8 @@ struct GridSrc {
   int64_t grid_size, first_grid, n_grids;
 };
 hipError_t launch_grid_stats(const GridSrc& g, ccka_grid_stats* out, hipStream_t s);
+// streaming 16-byte-per-lane device copy (the measured copy ceiling of bench.py)
+hipError_t launch_copy16(const void* in, void* out, int64_t bytes, int cus, hipStream_t s);
 // non-dominated entries of in[0..n) (n may be device-resident: *n_dev if n < 0),
 // compacted in input order into out; count into *count_dev
 hipError_t launch_pareto(const ccka_grid_stats* in, int n, const int32_t* n_dev, uint8_t* flags,

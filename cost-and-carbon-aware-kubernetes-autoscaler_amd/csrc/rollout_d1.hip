@@ -324,13 +324,21 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_LEAN_V 2
 #endif
 #ifndef D1_S_V
-#define D1_S_V 4
+#define D1_S_V 8
 #endif
 // LEAN 2: 1 = a proposal below cur held by the down window is a quiet step
 // (its record is rebuilt at the next event), 0 = such a step is an event, so
-// every quiet record is cur and the rebuild is a fill
+// every quiet record is cur and the rebuild is a fill (measured: 0 makes 21 %
+// of config 2's lane-steps events, 2x slower)
 #ifndef D1_HELD_V
-#define D1_HELD_V 0
+#define D1_HELD_V 1
+#endif
+// LEAN 2: quiet steps may cross one clock-hour boundary; the next event step
+// charges the hour that ended and starts the new one (prices, carbon
+// intensity) for them (not with replacement consolidation, whose offers are
+// re-evaluated at every hour)
+#ifndef D1_LAZYH_V
+#define D1_LAZYH_V 0
 #endif
 constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
 constexpr int D1_K = D1_K_V;      // event cadence (iterations)
@@ -496,11 +504,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
   int salloc[MAXN];     // alloc_cpu_m of the slot's type (< 2^24 by eligibility)
   int sallocr[MAXN];    // salloc once the node is ready, else 0
-  float sinv[MAXN];     // 1/alloc (saturation pre-test of the quiet step's energy)
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
     sinfo[n] = 0; sready[n] = 0; slc[n] = 0; scas[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
-    sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0; sinv[n] = 0.f;
+    sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0;
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
   // DRIFT (SEMANTICS 3.G0): drifted slots, sources of an in-flight pre-spun
@@ -572,6 +579,14 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int q_ulim = 0, q_pge = 0, q_slo = 0, q_usat = 0, q_w0 = 0, q_w1 = 0, q_pendv = 0, q_nodes = 0;
   float q_hbp = 0.f;   // 0.5 / ready pods (upp = (usage + 0.5) / ready pods, truncated)
   uint32_t usum = 0;   // sum of upp over the quiet steps since the last flush
+  // lazy hour crossing: th = the next clock-hour boundary step; quiet steps at
+  // or after it add their upp to usumB too (and a saturation correction to
+  // ecB); lazy_n2 (> 0 after a crossing) steps of node cost wait for the new
+  // hour's prices
+  constexpr bool LAZY_OK = BDEF && D1_LEAN_V == 2 && D1_LAZYH_V;
+  int th = 0x7fffffff, lazy_n2 = 0;
+  uint32_t usumB = 0;
+  long long ecB = 0;
   bool q_met = false;  // the HPA has a metric (records are proposals, else invalid)
 
   auto refresh_J = [&](int rh) {
@@ -721,11 +736,29 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // per-step constants of the quiet steps since the last event (SEMANTICS §3.H)
   auto flush = [&](int upto) {
     const int n = upto - tq;
-    cost += (burn + base_price) * (long long)n;
-    e_hour += (base_nw + Isum) * (long long)n;
-    if constexpr (BDEF && D1_LEAN_V == 2) {  // dynamic energy of the quiet steps (exact integers)
-      e_hour += (long long)(Ssum * (unsigned long long)usum);
+    if (LAZY_OK && th < upto) {
+      // the quiet steps crossed the hour boundary th: charge [tq, th) to the
+      // hour that ended (its carbon intensity is still loaded), start the new
+      // hour's energy with [th, upto); their node cost follows the reload of
+      // the new hour's prices (hchg)
+      const int n1 = th - tq, n2 = upto - th;
+      cost += (burn + base_price) * (long long)n1;
+      e_hour += (base_nw + Isum) * (long long)n1 + (long long)(Ssum * (unsigned long long)(usum - usumB));
+      gco2 += (double)e_hour * (ci_min * 1e-9);
+      energy_nw += e_hour;
+      e_hour = (base_nw + Isum) * (long long)n2 + (long long)(Ssum * (unsigned long long)usumB) + ecB;
+      hour = ((sm0 + th) % 1440) / 60;
+      lazy_n2 = n2;  // >= 1: also the "crossed" flag until the reload
       usum = 0;
+      usumB = 0;
+      ecB = 0;
+    } else {
+      cost += (burn + base_price) * (long long)n;
+      e_hour += (base_nw + Isum) * (long long)n;
+      if constexpr (BDEF && D1_LEAN_V == 2) {  // dynamic energy of the quiet steps (exact integers)
+        e_hour += (long long)(Ssum * (unsigned long long)usum);
+        usum = 0;
+      }
     }
     pend_min += (replicas - rpods) * n;
     nmin_spot += nsp * n;
@@ -815,35 +848,53 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               for (int j = 1; j < CCKA_HIST; ++j)
                 if (j <= kq) ring_push(hdn, rv);
             }
-          } else
-          if (kq > 0) {
+          } else if (kq > 0) {
+            // entry j of the rebuilt window = the record of step t-1-j (j < kq);
+            // the rows' samples are read first (independent LDS reads), held
+            // proposals are computed only in waves where some lane has one
             const int cur16 = min(replicas, D1_REC_SAT);
-            const int dreq = rpods * req;
-            const float rbd = __builtin_amdgcn_rcpf((float)dreq);
+            int us[CCKA_HIST], rv[CCKA_HIST];
+            bool anylow = false;
 #pragma unroll
-            for (int j = CCKA_HIST; j >= 1; --j) {
-              if (j <= kq) {
-                const int us = min(ring[((t - j) & (D1_RB - 1)) * WAVE + lane], q_rcap);
-                int rv = q_met ? cur16 : (int)0x8000;
-                if (q_met && us < q_pge) {
-                  // held below cur: util < ulo <= target, so no unready rule and the
-                  // proposal is ceil(util * ready / target) (binary64 at an exact
-                  // multiple, as the spec writes it); us < 2^20 and util < 2^15
-                  // keep both f32 quotients exact after one correction
-                  bool sl = false;
-                  const int util = fdiv_nb(us * 100, dreq, rbd, sl);
-                  const int x = (int)__umul24((uint32_t)util, (uint32_t)rpods);
-                  const int q = fdiv_nb(x, target, rtarget, sl);
-                  int c = q + (x == q * target ? 0 : 1);
-                  if (__builtin_expect(x == q * target, 0)) c = (int)ceil(((double)util / (double)target) * (double)rpods);
-                  rv = min(c, D1_REC_SAT);
-                }
-                ring_push(hdn, rv);
+            for (int j = 0; j < CCKA_HIST; ++j) {
+              us[j] = min(ring[((t - 1 - j) & (D1_RB - 1)) * WAVE + lane], q_rcap);
+              rv[j] = q_met ? cur16 : (int)0x8000;
+              anylow |= (j < kq) & q_met & (us[j] < q_pge);
+            }
+            if (anylow) {
+              // held below cur: util < ulo <= target, so no unready rule and the
+              // proposal is ceil(util * ready / target) (binary64 at an exact
+              // multiple, as the spec writes it); us < 2^20 and util < 2^15 keep
+              // both f32 quotients exact after one correction
+              const int dreq = rpods * req;
+              const float rbd = __builtin_amdgcn_rcpf((float)dreq);
+              bool anyex = false;
+#pragma unroll
+              for (int j = 0; j < CCKA_HIST; ++j) {
+                bool sl = false;
+                const bool low = (j < kq) & q_met & (us[j] < q_pge);
+                const int util = fdiv_nb(us[j] * 100, dreq, rbd, sl);
+                const int x = (int)__umul24((uint32_t)util, (uint32_t)rpods);
+                const int q = fdiv_nb(x, target, rtarget, sl);
+                const bool ex = x == q * target;
+                anyex |= low & ex;
+                rv[j] = low ? min(q + (ex ? 0 : 1), D1_REC_SAT) : rv[j];
+                us[j] = (low & ex) ? util : -1;  // exact multiples: the spec's binary64 below
+              }
+              if (__builtin_expect(anyex, 0)) {
+#pragma unroll
+                for (int j = 0; j < CCKA_HIST; ++j)
+                  if (us[j] >= 0)
+                    rv[j] = min((int)ceil(((double)us[j] / (double)target) * (double)rpods), D1_REC_SAT);
               }
             }
+#pragma unroll
+            for (int j = CCKA_HIST - 1; j >= 0; --j)
+              if (j < kq) ring_push(hdn, rv[j]);
           }
         }
         flush(t);
+        if (LAZY_OK && lazy_n2 > 0) hchg = true;  // quiet steps crossed into this hour: load its prices below
         minute = (sm0 + t) % 1440;
         const int h = minute / 60;
         rh = r * 24 + h;
@@ -995,6 +1046,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               burn += np[n];
             }
           }
+          if constexpr (LAZY_OK) {  // node cost of the quiet steps since the lazy crossing
+            cost += (burn + base_price) * (long long)lazy_n2;
+            lazy_n2 = 0;
+          }
         }
         if (hchg || jchg) refresh_J(rh);
         // ---- F2. Karpenter provisioning: claims of min(J, pending) pods ----
@@ -1032,7 +1087,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                     sdyn[n] = (uint32_t)ac.z;
                     salloc[n] = ac.w;
                     sallocr[n] = delay == 0 ? ac.w : 0;
-                    sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
                   }
                 }
                 const uint32_t bit = 1u << slot;
@@ -1239,7 +1293,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                       sdyn[n] = (uint32_t)ac.z;
                       salloc[n] = ac.w;
                       sallocr[n] = delay == 0 ? ac.w : 0;
-                      sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
                     }
                     if (n == best) spods[n] = need;
                   }
@@ -1411,7 +1464,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                       sdyn[n] = (uint32_t)ac.z;
                       salloc[n] = ac.w;
                       sallocr[n] = delay == 0 ? ac.w : 0;
-                      sinv[n] = __builtin_amdgcn_rcpf((float)ac.w);
                     }
                   }
                   const uint32_t bit = 1u << slot;
@@ -1459,7 +1511,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           for (int n = 0; n < MAXN; ++n) {
             const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] : 0u;
             sv += (unsigned long long)sdyn[n] * pr;
-            rv = fmaxf(rv, (float)pr * sinv[n]);
+            rv = fmaxf(rv, (float)pr * __builtin_amdgcn_rcpf((float)salloc[n]));  // 1/alloc only here
           }
           Ssum = sv;
           Rmax = rv;
@@ -1593,7 +1645,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // with the same candidates), or the next step when disruption acted
         // (the budget may allow more)
         {
-          int nx = min(next_ready, t + 60 - minute % 60);
+          th = t + 60 - minute % 60;  // the next clock-hour boundary
+          // lazy: quiet steps may cross it, but the event that charges the
+          // crossing must fall inside the new hour (its prices load there)
+          int nx = min(next_ready, (LAZY_OK && !(DRIFT && replace)) ? th + 59 : th);
           if (pswitch) {
             if (t >= npb) {  // the next peak-window boundary
               const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;
@@ -1656,9 +1711,13 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         stall = stall | (can & !ok);
         if constexpr (D1_HELD_V) q_hold = (go & ge) ? max(q_hold, t + wl) : q_hold;
         const int upp = (int)fmaf((float)usage, q_rbp, q_hbp);
-        if (__builtin_expect(go & (upp > q_usat), 0))  // a node may saturate: exact per-node sum instead
-          e_hour += dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+        if (__builtin_expect(go & (upp > q_usat), 0)) {  // a node may saturate: exact per-node sum instead
+          const long long corr = dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+          if (LAZY_OK && t >= th) ecB += corr;
+          else e_hour += corr;
+        }
         usum += go ? (uint32_t)upp : 0u;
+        if constexpr (LAZY_OK) usumB += (go & (t >= th)) ? (uint32_t)upp : 0u;
         const bool slo_b = usage >= q_slo;
         slo += (go & slo_b) ? 1 : 0;
         d1_store_rec(trs, go ? lb + t * 16 : D1_NOSTORE, make_int4(replicas, q_pendv, q_nodes, slo_b ? q_w1 : q_w0));
@@ -1771,6 +1830,18 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
   }
   flush(T);
+  if (LAZY_OK && lazy_n2 > 0) {  // the last quiet steps crossed into a new hour: its prices and carbon intensity
+    const int rh = r * 24 + hour;
+    const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
+    ci_min = ci_gpwmin[rh];
+    long long b = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n) {
+      const uint32_t x = sinfo[n];
+      if (used >> n & 1u) b += tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
+    }
+    cost += b * (long long)lazy_n2;
+  }
   energy_nw += e_hour;
   gco2 += (double)e_hour * (ci_min * 1e-9);
   p.cost[i] = cost;

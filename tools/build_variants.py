@@ -16,11 +16,14 @@ subprocess.run(["make", "-s", "-C", CSRC], check=True)
 procs = []
 for arg in sys.argv[1:]:
     name, _, defs = arg.partition("=")
+    src = "rollout_d1.hip"
+    if defs.startswith("@"):  # NAME=@other.hip[:flags]: another source file in csrc/ (e.g. a committed version)
+        src, _, defs = defs[1:].partition(":")
     out = os.path.join(CSRC, "build", "variants", name)
     os.makedirs(out, exist_ok=True)
     obj = os.path.join(out, "rollout_d1.o")
     procs.append((name, out, obj, subprocess.Popen(["/opt/rocm/bin/hipcc", *FLAGS, *defs.split(), "-c", "-o", obj,
-                                                    os.path.join(CSRC, "rollout_d1.hip")])))
+                                                    os.path.join(CSRC, src)])))
 for name, out, obj, p in procs:
     assert p.wait() == 0, name
     others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "sweep.o", "mlp.o", "ccka_abi.o")]
