@@ -303,6 +303,16 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu:
             out["cpu_baseline"], out["parity"], out["parity_detail"] = cpu_baseline(
                 eng, spec, sc, args.cpu_seconds, traj, local_totals)
+        elif world > 1 and not args.no_cpu:
+            # every rank: an untimed prefix of its own shard against the oracle
+            ok, det = rank_parity(eng, spec, sc, traj)
+            flags = [None] * world
+            dist.all_gather_object(flags, (rank, ok, det))
+            if rank == 0:
+                out["parity"] = all(f[1] for f in flags)
+                out["parity_detail"] = {"per_rank": [f[2] for f in flags],
+                                        "rule": "per rank: the first scenarios of its shard, results (and "
+                                                "trajectory) bit-exact vs the CPU oracle on the same traces"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
@@ -471,6 +481,24 @@ def cpu_baseline(eng, spec, sc, target_s, traj, gpu_totals):
             "value_nproc_threads": None if tn is None else n * T / tn,
             "build": f"gcc -O3 -march={march} -ffp-contract=off"}
     return base, parity, detail
+
+
+def rank_parity(eng, spec, sc, traj, n=10_000):
+    """Untimed check of this rank's shard prefix (global ids first_id ..
+    first_id + n) against the CPU oracle on the same device-generated traces:
+    every per-scenario result and, in trajectory mode, every record."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+
+    n = min(n, sc.n)
+    load = eng.get_load()
+    ld = load if sc.n_traces else np.ascontiguousarray(load[:, :, :n])
+    ref, ref_tr = po.rollout(spec, sc.slice(0, n), ld, traj=traj, threads=max(1, min(16, os.cpu_count() or 1)))
+    got = eng.results()
+    bad = [k for k in ref if not np.array_equal(got[k][:n], ref[k])]
+    if traj and not np.array_equal(eng.trajectory()[:, :n], ref_tr):
+        bad.append("trajectory")
+    return not bad, {"first_id": int(sc.first_id), "scenarios": n, "mismatched": bad}
 
 
 def abi_totals_fields():

@@ -122,6 +122,20 @@ class Totals(C.Structure):
                 ("energy_wmin", C.c_double), ("gco2", C.c_double)]
 
 
+class PgParams(C.Structure):
+    """ccka_pg_params: the stochastic closed loop's sampling key and objective weights."""
+    _fields_ = [("seed", C.c_uint64), ("w_carbon", C.c_double), ("w_slo", C.c_double),
+                ("baseline", C.c_int32), ("_pad", C.c_int32)]
+
+
+class MlpGrads(C.Structure):
+    """ccka_mlp_grads: fp32 host gradient arrays (layouts of ccka_mlp_set_weights)."""
+    _fields_ = [(n, C.POINTER(C.c_float)) for n in ("w1", "b1", "w2", "b2", "w3", "b3")]
+
+
+GRAD_SHAPES = {"w1": (64, 256), "b1": (256,), "w2": (256, 256), "b2": (256,), "w3": (256, 8), "b3": (8,)}
+
+
 class GridStats(C.Structure):
     _fields_ = [("grid", C.c_int64), ("scenarios", C.c_int64), ("cost_uphmin", C.c_int64),
                 ("slo_minutes", C.c_int64), ("gco2", C.c_double), ("energy_wmin", C.c_double)]
@@ -221,6 +235,10 @@ def load_engine(path: str | None = None):
         "ccka_policy_rollout": (C.c_int, [vp, C.c_int32, C.c_int32]),
         "ccka_get_policy_actions": (C.c_int, [vp, C.c_void_p, C.c_void_p, C.c_int64]),
         "ccka_get_detail": (C.c_int, [vp, C.c_void_p, C.c_int64]),
+        "ccka_policy_grad": (C.c_int, [vp, C.POINTER(PgParams), C.POINTER(MlpGrads), C.POINTER(C.c_double)]),
+        "ccka_get_policy_samples": (C.c_int, [vp, C.POINTER(C.c_uint8), C.POINTER(C.c_float), C.c_int64]),
+        "ccka_mlp_backward": (C.c_int, [vp, C.POINTER(C.c_uint16), C.POINTER(C.c_uint8), C.POINTER(C.c_float),
+                                        C.c_int64, C.POINTER(MlpGrads)]),
         "ccka_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "ccka_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
         "ccka_allreduce_totals": (C.c_int, [vp, C.POINTER(Totals)]),
@@ -245,6 +263,7 @@ EXPORTED = [
     "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
     "ccka_mlp_forward_async", "ccka_mlp_get_actions", "ccka_set_detail", "ccka_get_detail",
     "ccka_policy_rollout", "ccka_get_policy_actions", "ccka_trajectory_layout", "ccka_get_trajectory_native",
+    "ccka_policy_grad", "ccka_get_policy_samples", "ccka_mlp_backward",
 ]
 TRAJ_TN, TRAJ_NT = 0, 1  # device layouts of the trajectory records (ccka_trajectory_layout)
 

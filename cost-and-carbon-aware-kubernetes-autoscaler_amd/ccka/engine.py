@@ -107,6 +107,42 @@ class Engine:
                                                       None), "ccka_get_trajectory_native")
         return a, lay.value
 
+    @staticmethod
+    def _grads():
+        g = {k: np.zeros(v, np.float32) for k, v in abi.GRAD_SHAPES.items()}
+        s = abi.MlpGrads(*[g[k].ctypes.data_as(C.POINTER(C.c_float)) for k in ("w1", "b1", "w2", "b2", "w3", "b3")])
+        return g, s
+
+    def policy_grad(self, seed: int, w_carbon: float = 0.0, w_slo: float = 0.0, baseline: bool = True):
+        """One stochastic closed-loop rollout and the score-function gradient
+        of E[J] (ccka_policy_grad): (grads dict, mean objective)."""
+        g, s = self._grads()
+        prm = abi.PgParams(seed, w_carbon, w_slo, int(bool(baseline)), 0)
+        obj = C.c_double()
+        self._chk(self.lib.ccka_policy_grad(self.ctx, C.byref(prm), C.byref(s), C.byref(obj)), "ccka_policy_grad")
+        return g, obj.value
+
+    def policy_samples(self):
+        """(actions [T][N] uint8, coef [N] fp32) of the last policy_grad."""
+        a = np.zeros((self.T, self.n), np.uint8)
+        cf = np.zeros(self.n, np.float32)
+        self._chk(self.lib.ccka_get_policy_samples(self.ctx, a.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                   cf.ctypes.data_as(C.POINTER(C.c_float)), a.size),
+                  "ccka_get_policy_samples")
+        return a, cf
+
+    def mlp_backward(self, x_bits: np.ndarray, actions: np.ndarray, coef: np.ndarray):
+        """Gradient of sum_m coef[m] log softmax(policy(x_m))[a_m] (ccka_mlp_backward)."""
+        x = np.ascontiguousarray(x_bits, np.uint16)
+        a = np.ascontiguousarray(actions, np.uint8)
+        cf = np.ascontiguousarray(coef, np.float32)
+        g, s = self._grads()
+        self._chk(self.lib.ccka_mlp_backward(self.ctx, x.ctypes.data_as(C.POINTER(C.c_uint16)),
+                                             a.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                             cf.ctypes.data_as(C.POINTER(C.c_float)), len(a), C.byref(s)),
+                  "ccka_mlp_backward")
+        return g
+
     def totals(self) -> abi.Totals:
         t = abi.Totals()
         self._chk(self.lib.ccka_get_totals(self.ctx, C.byref(t)), "ccka_get_totals")

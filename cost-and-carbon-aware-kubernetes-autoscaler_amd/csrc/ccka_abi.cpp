@@ -136,6 +136,22 @@ struct ccka_ctx {
   bool pol_feat_on = false;
   uint16_t* d_feat_rec = nullptr;
   int64_t pol_feat_count = 0;
+  // differentiable control (ccka_policy_grad / ccka_mlp_backward, pg.hip)
+  mlp_bf16x8* d_w2b = nullptr;   // A fragments of dH1^T = W2 dH2^T
+  mlp_bf16x8* d_w3b = nullptr;   // A fragments of dH2^T = W3 g_y^T
+  uint8_t* d_pg_act = nullptr;   // sampled actions [T][N] (or the rows of ccka_mlp_backward)
+  int64_t pg_act_count = 0;
+  float* d_pg_coef = nullptr;    // per-scenario (J - b) / N (or per row)
+  int64_t pg_coef_count = 0;
+  uint16_t* d_pg_x = nullptr;    // ccka_mlp_backward's rows [M][64]
+  int64_t pg_x_count = 0;
+  uint16_t* d_pg_work = nullptr; // xT | h1T | h2T | dh1T | dh2T | gyT | ones, each [rows][Mpad]
+  int64_t pg_work_count = 0;
+  float* d_pg_part = nullptr;    // weight-gradient row-split partials
+  int64_t pg_part_count = 0;
+  float* d_pg_grad = nullptr;    // dW1 | db1 | dW2 | db2 | dW3 | db3
+  bool pg_valid = false;
+  int64_t pg_T = 0;
   // per-scenario summary breakdown (ccka_set_detail)
   bool detail_on = false;
   bool detail_valid = false;
@@ -534,6 +550,8 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_pol_state); dfree(c->d_pol_target); dfree(c->d_pol_cw); dfree(c->d_rec_target); dfree(c->d_rec_cw);
   dfree(c->d_feat_rec);
   dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
+  dfree(c->d_w2b); dfree(c->d_w3b); dfree(c->d_pg_act); dfree(c->d_pg_coef); dfree(c->d_pg_x);
+  dfree(c->d_pg_work); dfree(c->d_pg_part); dfree(c->d_pg_grad);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1055,8 +1073,13 @@ static int64_t state_words(int dmax, int nmax) {
   return (int64_t)dmax * (5 + 2 * CCKA_HIST) + 5 * CCKA_MAX_POOLS + (int64_t)nmax * (6 + dmax) + 36;
 }
 
-int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
+// The closed loop (SEMANTICS 5). pg == nullptr: the deterministic policy
+// (policy_act_kernel); otherwise each step samples an action bin from
+// softmax(y) (policy_sample_kernel) and the features and actions of every
+// step are kept for the score-function gradient (ccka_policy_grad).
+static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const ccka_pg_params* pg) {
   if (!c) return CCKA_EINVAL;
+  c->pg_valid = false;  // the recorded features / actions are about to be overwritten
   if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
   if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
   if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
@@ -1097,7 +1120,16 @@ int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
       c->pol_rec_count = (int64_t)T * N;
     }
   }
-  if (c->pol_feat_on) {
+  const bool feat_on = c->pol_feat_on || pg;
+  if (pg) {
+    if (c->pg_act_count < (int64_t)T * N) {
+      dfree(c->d_pg_act);
+      if (hipMalloc((void**)&c->d_pg_act, (size_t)T * N) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "policy-gradient action record alloc");
+      c->pg_act_count = (int64_t)T * N;
+    }
+  }
+  if (feat_on) {
     if (c->pol_feat_count < (int64_t)(T + 1) * N * 64) {
       dfree(c->d_feat_rec);
       if (hipMalloc((void**)&c->d_feat_rec, (size_t)(T + 1) * N * 64 * 2) != hipSuccess)
@@ -1123,7 +1155,7 @@ int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
   k.state = c->d_pol_state;
   k.feat = c->d_mx;
   auto keep_feat = [&](int t) -> int {
-    if (!c->pol_feat_on) return CCKA_OK;
+    if (!feat_on) return CCKA_OK;
     HIPCHK(c, hipMemcpyAsync(c->d_feat_rec + (size_t)t * N * 64, c->d_mx, (size_t)N * 64 * 2, hipMemcpyDeviceToDevice,
                              c->stream));
     return CCKA_OK;
@@ -1138,8 +1170,24 @@ int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
   if ((rc = keep_feat(0)) != CCKA_OK) return rc;
   for (int t = 0; t < T; ++t) {
     HIPCHK(c, launch_mlp(mp, c->cus, c->stream));
-    HIPCHK(c, launch_policy_act(c->d_my, c->d_pol_target, c->d_pol_cw, record ? c->d_rec_target + (size_t)t * N : nullptr,
-                                record ? c->d_rec_cw + (size_t)t * N : nullptr, N, c->stream));
+    if (pg) {
+      PgSampleParams q{};
+      q.y = c->d_my;
+      q.act = c->d_pg_act + (size_t)t * N;
+      q.target = c->d_pol_target;
+      q.cw = c->d_pol_cw;
+      q.rec_target = record ? c->d_rec_target + (size_t)t * N : nullptr;
+      q.rec_cw = record ? c->d_rec_cw + (size_t)t * N : nullptr;
+      q.n = N;
+      q.first_id = c->first_id;
+      q.seed = pg->seed;
+      q.t = t;
+      HIPCHK(c, launch_policy_sample(q, c->stream));
+    } else {
+      HIPCHK(c, launch_policy_act(c->d_my, c->d_pol_target, c->d_pol_cw,
+                                  record ? c->d_rec_target + (size_t)t * N : nullptr,
+                                  record ? c->d_rec_cw + (size_t)t * N : nullptr, N, c->stream));
+    }
     k.t0 = t;
     k.t1 = t + 1;
     k.state_load = 1;
@@ -1164,6 +1212,195 @@ int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
   return ccka_sync(c);
 }
 
+int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
+  return policy_loop(c, trajectory, record, nullptr);
+}
+
+// ---- differentiable control: the MLP backward (pg.hip) ----
+// rows m = 0..M-1 of x [M][64] bf16 / act [M] / coef[m % n_scen] -> d_pg_grad
+// (dW1 | db1 | dW2 | db2 | dW3 | db3, fp32, the layouts of ccka_mlp_set_weights)
+static constexpr int64_t kGradFloats = 64 * 256 + 256 + 256 * 256 + 256 + 256 * 8 + 8;
+static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const float* coef, int64_t n_scen,
+                       int64_t M) {
+  if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
+  if (M < 1 || n_scen < 1) return fail(c, CCKA_EINVAL, "no rows");
+  const int64_t Mpad = (M + 31) / 32 * 32;
+  const int64_t rows = 64 + 4 * MLP_HID + 8 + 1;  // xT h1T h2T dh1T dh2T gyT ones
+  if (c->pg_work_count < rows * Mpad) {
+    dfree(c->d_pg_work);
+    c->pg_work_count = 0;
+    if (hipMalloc((void**)&c->d_pg_work, (size_t)(rows * Mpad) * 2) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "policy-gradient work alloc (%lld rows x %lld)", (long long)rows, (long long)Mpad);
+    c->pg_work_count = rows * Mpad;
+  }
+  if (!c->d_pg_grad && hipMalloc((void**)&c->d_pg_grad, (size_t)kGradFloats * 4) != hipSuccess)
+    return fail(c, CCKA_ENOMEM, "gradient alloc");
+  uint16_t* xT = c->d_pg_work;
+  uint16_t* h1T = xT + 64 * Mpad;
+  uint16_t* h2T = h1T + MLP_HID * Mpad;
+  uint16_t* dh1T = h2T + MLP_HID * Mpad;
+  uint16_t* dh2T = dh1T + MLP_HID * Mpad;
+  uint16_t* gyT = dh2T + MLP_HID * Mpad;
+  uint16_t* ones = gyT + 8 * Mpad;
+  HIPCHK(c, launch_pg_fill(ones, Mpad, M, 0x3F80 /* bf16 1.0 */, c->stream));
+  PgRowsParams rp{};
+  rp.x = x;
+  rp.act = act;
+  rp.coef = coef;
+  rp.w1f = c->d_w1f;
+  rp.w2f = c->d_w2f;
+  rp.w3f = c->d_w3f;
+  rp.w2b = c->d_w2b;
+  rp.w3b = c->d_w3b;
+  rp.bias = c->d_mb;
+  rp.xT = xT; rp.h1T = h1T; rp.h2T = h2T; rp.dh1T = dh1T; rp.dh2T = dh2T; rp.gyT = gyT;
+  rp.M = M;
+  rp.Mpad = Mpad;
+  rp.n_scen = n_scen;
+  HIPCHK(c, launch_pg_rows(rp, c->cus, c->stream));
+  // the six reductions over rows; row splits fill the chip, >= 256 rows each,
+  // fixed for a given Mpad (deterministic sums)
+  struct G { const uint16_t* a; int ka; const uint16_t* b; int kb; int64_t off; };
+  const int64_t o_b1 = 64 * 256, o_w2 = o_b1 + 256, o_b2 = o_w2 + 256 * 256, o_w3 = o_b2 + 256, o_b3 = o_w3 + 256 * 8;
+  const G gs[6] = {{xT, 64, dh1T, MLP_HID, 0}, {dh1T, MLP_HID, ones, 1, o_b1}, {h1T, MLP_HID, dh2T, MLP_HID, o_w2},
+                   {dh2T, MLP_HID, ones, 1, o_b2}, {h2T, MLP_HID, gyT, MLP_OUT, o_w3}, {gyT, MLP_OUT, ones, 1, o_b3}};
+  auto splits_of = [&](const G& g) {
+    const int64_t tiles = (int64_t)((g.ka + 31) / 32) * ((g.kb + 31) / 32);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(2048 / tiles, Mpad / 256));
+  };
+  int64_t need = 0;
+  for (const G& g : gs) need = std::max<int64_t>(need, (int64_t)splits_of(g) * g.ka * g.kb);
+  if (c->pg_part_count < need) {
+    dfree(c->d_pg_part);
+    c->pg_part_count = 0;
+    if (hipMalloc((void**)&c->d_pg_part, (size_t)need * 4) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "gradient partials alloc");
+    c->pg_part_count = need;
+  }
+  for (const G& g : gs) {
+    WgradParams q{};
+    q.A = g.a;
+    q.B = g.b;
+    q.part = c->d_pg_part;
+    q.Mpad = Mpad;
+    q.KA = g.ka;
+    q.KB = g.kb;
+    q.splits = splits_of(g);
+    HIPCHK(c, launch_pg_wgrad(q, c->d_pg_grad + g.off, c->stream));
+  }
+  return CCKA_OK;
+}
+
+static int pg_copy_grads(ccka_ctx* c, ccka_mlp_grads* out) {
+  if (!out) return CCKA_OK;
+  const int64_t o_b1 = 64 * 256, o_w2 = o_b1 + 256, o_b2 = o_w2 + 256 * 256, o_w3 = o_b2 + 256, o_b3 = o_w3 + 256 * 8;
+  const struct { float* dst; int64_t off, n; } m[6] = {{out->w1, 0, 64 * 256}, {out->b1, o_b1, 256},
+                                                      {out->w2, o_w2, 256 * 256}, {out->b2, o_b2, 256},
+                                                      {out->w3, o_w3, 256 * 8}, {out->b3, o_b3, 8}};
+  for (const auto& x : m)
+    if (x.dst) HIPCHK(c, hipMemcpyAsync(x.dst, c->d_pg_grad + x.off, (size_t)x.n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
+int ccka_mlp_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* actions, const float* coef, int64_t m,
+                      ccka_mlp_grads* out) {
+  if (!c || !x || !actions || !coef || !out || m < 1) return CCKA_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (c->pg_x_count < m * MLP_IN) {
+    dfree(c->d_pg_x);
+    c->pg_x_count = 0;
+    if (hipMalloc((void**)&c->d_pg_x, (size_t)m * MLP_IN * 2) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "backward rows alloc");
+    c->pg_x_count = m * MLP_IN;
+  }
+  if (c->pg_act_count < m) {
+    dfree(c->d_pg_act);
+    c->pg_act_count = 0;
+    if (hipMalloc((void**)&c->d_pg_act, (size_t)m) != hipSuccess) return fail(c, CCKA_ENOMEM, "action alloc");
+    c->pg_act_count = m;
+  }
+  if (c->pg_coef_count < m) {
+    dfree(c->d_pg_coef);
+    c->pg_coef_count = 0;
+    if (hipMalloc((void**)&c->d_pg_coef, (size_t)m * 4) != hipSuccess) return fail(c, CCKA_ENOMEM, "coef alloc");
+    c->pg_coef_count = m;
+  }
+  for (int64_t i = 0; i < m; ++i)
+    if (actions[i] >= MLP_OUT) return fail(c, CCKA_EINVAL, "action %d of row %lld out of range", actions[i], (long long)i);
+  HIPCHK(c, hipMemcpyAsync(c->d_pg_x, x, (size_t)m * MLP_IN * 2, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_pg_act, actions, (size_t)m, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_pg_coef, coef, (size_t)m * 4, hipMemcpyHostToDevice, c->stream));
+  c->pg_valid = false;  // the recorded samples of ccka_policy_grad are gone
+  int rc;
+  if ((rc = pg_backward(c, c->d_pg_x, c->d_pg_act, c->d_pg_coef, m, m)) != CCKA_OK) return rc;
+  return pg_copy_grads(c, out);
+}
+
+int ccka_policy_grad(ccka_ctx* c, const ccka_pg_params* pg, ccka_mlp_grads* out, double* objective_mean) {
+  if (!c || !pg) return CCKA_EINVAL;
+  if (!(pg->w_carbon >= 0.0) || !(pg->w_slo >= 0.0)) return fail(c, CCKA_EINVAL, "objective weights must be >= 0");
+  (void)hipSetDevice(c->device);
+  int rc;
+  if ((rc = policy_loop(c, 0, 1, pg)) != CCKA_OK) return rc;
+  const int64_t N = c->N;
+  const int64_t T = c->hw.n_steps;
+  // J_i = cost $ + w_c gCO2 kg + w_s SLO minutes; coef_i = (J_i - b) / N
+  std::vector<int64_t> cost((size_t)N);
+  std::vector<double> g((size_t)N);
+  std::vector<int32_t> slo((size_t)N);
+  HIPCHK(c, hipMemcpyAsync(cost.data(), c->kp.cost, (size_t)N * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(g.data(), c->kp.gco2, (size_t)N * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(slo.data(), c->kp.slo, (size_t)N * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<double> J((size_t)N);
+  double sum = 0.0;
+  for (int64_t i = 0; i < N; ++i) {
+    J[(size_t)i] = (double)cost[(size_t)i] / 6e7 + pg->w_carbon * (g[(size_t)i] * 1e-3) + pg->w_slo * (double)slo[(size_t)i];
+    sum += J[(size_t)i];
+  }
+  const double mean = sum / (double)N, b = pg->baseline ? mean : 0.0;
+  std::vector<float> coef((size_t)N);
+  for (int64_t i = 0; i < N; ++i) coef[(size_t)i] = (float)((J[(size_t)i] - b) / (double)N);
+  if (objective_mean) *objective_mean = mean;
+  if (c->pg_coef_count < N) {
+    dfree(c->d_pg_coef);
+    c->pg_coef_count = 0;
+    if (hipMalloc((void**)&c->d_pg_coef, (size_t)N * 4) != hipSuccess) return fail(c, CCKA_ENOMEM, "coef alloc");
+    c->pg_coef_count = N;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_pg_coef, coef.data(), (size_t)N * 4, hipMemcpyHostToDevice, c->stream));
+  // rows (t, i) -> m = t N + i: the recorded features [T+1][N][64] (steps 0..T-1) and actions [T][N]
+  if ((rc = pg_backward(c, c->d_feat_rec, c->d_pg_act, c->d_pg_coef, N, T * N)) != CCKA_OK) return rc;
+  c->pg_valid = true;
+  c->pg_T = T;
+  return pg_copy_grads(c, out);
+}
+
+// Internal (tests): the backward's unit-major work arrays of the last
+// ccka_mlp_backward / ccka_policy_grad: xT | h1T | h2T | dh1T | dh2T | gyT |
+// ones, each [rows][Mpad] bf16; *mpad receives Mpad.
+int ccka_debug_pg_work(ccka_ctx* c, uint16_t* out, int64_t count, int64_t* mpad) {
+  if (!c || !out || !mpad || !c->d_pg_work) return CCKA_EINVAL;
+  const int64_t rows = 64 + 4 * MLP_HID + 8 + 1;
+  if (count < c->pg_work_count) return fail(c, CCKA_EINVAL, "need %lld", (long long)c->pg_work_count);
+  (void)hipSetDevice(c->device);
+  *mpad = c->pg_work_count / rows;
+  HIPCHK(c, hipMemcpy(out, c->d_pg_work, (size_t)c->pg_work_count * 2, hipMemcpyDeviceToHost));
+  return CCKA_OK;
+}
+
+int ccka_get_policy_samples(ccka_ctx* c, uint8_t* actions, float* coef, int64_t count) {
+  if (!c || !actions || !coef) return CCKA_EINVAL;
+  if (!c->pg_valid) return fail(c, CCKA_ESTATE, "no ccka_policy_grad samples");
+  if (count != c->pg_T * c->N) return fail(c, CCKA_EINVAL, "sample count mismatch");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipMemcpyAsync(actions, c->d_pg_act, (size_t)count, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(coef, c->d_pg_coef, (size_t)c->N * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return CCKA_OK;
+}
+
 int ccka_get_policy_actions(ccka_ctx* c, int16_t* target, double* cw, int64_t count) {
   if (!c || !target || !cw) return CCKA_EINVAL;
   if (!c->pol_rec_valid) return fail(c, CCKA_ESTATE, "last run recorded no policy actions");
@@ -1185,7 +1422,7 @@ int ccka_debug_policy_features(ccka_ctx* c, int32_t enable) {
 
 int ccka_debug_get_policy_features(ccka_ctx* c, uint16_t* out, int64_t count) {
   if (!c || !out) return CCKA_EINVAL;
-  if (!c->pol_feat_on || !c->pol_rec_valid) return fail(c, CCKA_ESTATE, "no recorded features");
+  if (!(c->pol_feat_on || c->pg_valid) || !c->pol_rec_valid) return fail(c, CCKA_ESTATE, "no recorded features");
   if (count != (int64_t)(c->hw.n_steps + 1) * c->N * 64) return fail(c, CCKA_EINVAL, "feature count mismatch");
   (void)hipSetDevice(c->device);
   HIPCHK(c, hipMemcpyAsync(out, c->d_feat_rec, (size_t)count * 2, hipMemcpyDeviceToHost, c->stream));
@@ -1495,6 +1732,22 @@ int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t ou
         const int r = l & 31, h = l >> 5;
         if (r < MLP_OUT) f3[((size_t)kk * 64 + l) * 8 + j] = w3[(size_t)kin(kk, j, h) * MLP_OUT + r];
       }
+  // backward (pg.hip): dH1^T = W2 dH2^T with dH2^T chained in the same permuted
+  // k order (rows = H1 units), dH2^T = W3 g_y^T with k = action padded to 16
+  std::vector<uint16_t> f2b((size_t)8 * 16 * 64 * 8), f3b((size_t)8 * 64 * 8, 0);
+  for (int n = 0; n < 8; ++n)
+    for (int kk = 0; kk < 16; ++kk)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int r = l & 31, h = l >> 5;
+          f2b[(((size_t)n * 16 + kk) * 64 + l) * 8 + j] = w2[(size_t)(32 * n + r) * MLP_HID + kin(kk, j, h)];
+        }
+  for (int n = 0; n < 8; ++n)
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 8; ++j) {
+        const int r = l & 31, h = l >> 5;
+        if (h == 0) f3b[((size_t)n * 64 + l) * 8 + j] = w3[(size_t)(32 * n + r) * MLP_OUT + j];
+      }
   std::vector<float> bias(MLP_HID * 2 + 32);  // b3 zero-padded to one 32-row tile
   std::memcpy(bias.data(), b1, MLP_HID * 4);
   std::memcpy(bias.data() + MLP_HID, b2, MLP_HID * 4);
@@ -1504,6 +1757,8 @@ int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t ou
   if ((rc = dupload(c, c->d_w2f, (const mlp_bf16x8*)f2.data(), f2.size() / 8)) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_w3f, (const mlp_bf16x8*)f3.data(), f3.size() / 8)) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_mb, bias.data(), bias.size())) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w2b, (const mlp_bf16x8*)f2b.data(), f2b.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w3b, (const mlp_bf16x8*)f3b.data(), f3b.size() / 8)) != CCKA_OK) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->mlp_have_w = true;
   return CCKA_OK;

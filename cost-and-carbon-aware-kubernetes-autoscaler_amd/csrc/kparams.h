@@ -267,6 +267,49 @@ hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipS
 hipError_t launch_policy_act(const float* y, int16_t* target, double* cw, int16_t* rec_target, double* rec_cw,
                              int64_t n, hipStream_t s);
 hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Differentiable control: score-function policy gradient (pg.hip)
+// ---------------------------------------------------------------------------
+// one stochastic policy step: action ~ softmax(y) (Philox(seed; id, t)), mapped
+// to the step's HPA target and carbon weight (SEMANTICS 5)
+struct PgSampleParams {
+  const float* y;        // [n][8]
+  uint8_t* act;          // [n]
+  int16_t* target;       // [n]
+  double* cw;            // [n]
+  int16_t* rec_target;   // nullable [n]
+  double* rec_cw;        // nullable [n]
+  int64_t n, first_id;
+  uint64_t seed;
+  int32_t t, _pad;
+};
+hipError_t launch_policy_sample(const PgSampleParams& q, hipStream_t s);
+// forward recompute + backward per 32-row tile: unit-major [unit][Mpad] bf16 outputs
+struct PgRowsParams {
+  const uint16_t* x;        // [M][64] bf16
+  const uint8_t* act;       // [M]
+  const float* coef;        // [n_scen]: row m's factor is coef[m % n_scen]
+  const mlp_bf16x8* w1f;    // forward fragments (as MlpParams)
+  const mlp_bf16x8* w2f;
+  const mlp_bf16x8* w3f;
+  const mlp_bf16x8* w2b;    // [8 row blocks][16 k-steps][64]: A fragments of dH1^T = W2 dH2^T
+  const mlp_bf16x8* w3b;    // [8][64]: A fragments of dH2^T = W3 g_y^T (k = action, padded to 16)
+  const float* bias;        // b1 | b2 | b3 (zero-padded), as MlpParams
+  uint16_t *xT, *h1T, *h2T, *dh1T, *dh2T, *gyT;  // [64|256|256|256|256|8][Mpad]
+  int64_t M, Mpad, n_scen;
+};
+hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s);
+// C[KA][KB] = sum_m A[a][m] B[b][m] over unit-major bf16 operands (fp32 result)
+struct WgradParams {
+  const uint16_t* A;  // [KA][Mpad]
+  const uint16_t* B;  // [KB][Mpad]
+  float* part;        // [splits][KA][KB]
+  int64_t Mpad;
+  int32_t KA, KB, splits, _pad;
+};
+hipError_t launch_pg_wgrad(const WgradParams& q, float* out, hipStream_t s);
+hipError_t launch_pg_fill(uint16_t* x, int64_t n, int64_t valid, uint16_t v, hipStream_t s);
 // [N][T] (single-deployment engine, device side) -> steps [t0, t0 + tc) of the
 // [T][N] order ccka_get_trajectory returns, into out[tc][N]
 hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, int64_t N, int64_t T, int64_t t0,

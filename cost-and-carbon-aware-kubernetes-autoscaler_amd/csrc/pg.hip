@@ -1,0 +1,379 @@
+// pg.hip — differentiable control for the learned policy (BASELINE config 5,
+// "differentiable-control rollout"): a score-function (likelihood-ratio)
+// gradient of the closed loop's objective with respect to the MLP weights.
+//
+// The rollout's dynamics are integer and piecewise constant, so the objective
+// J = cost + w_c gCO2 + w_s SLO has no useful pathwise derivative. The policy
+// is made stochastic instead: at every step each scenario samples one of the
+// 8 action bins from softmax(y) (counter-based Philox, reproducible), and
+//   grad E[J] = E[(J - b) sum_t grad log pi(a_t | x_t)],
+// whose per-row factor is the softmax cross-entropy gradient
+// g_y = c (e_a - softmax(y)) with c = (J - b) / N. The MLP backward then runs
+// on bf16 MFMA with fp32 accumulation:
+//   pg_rows_kernel   recomputes H1, H2, y per 32-state tile (the forward's
+//                    transposed formulation), forms g_y, and back-propagates
+//                    dH2^T = W3 g_y^T (masked by H2 > 0) and dH1^T = W2 dH2^T
+//                    (masked by H1 > 0) with the same in-register operand
+//                    chaining; it stores X^T, H1^T, H2^T, dH1^T, dH2^T, g_y^T
+//                    unit-major ([unit][row], rows padded to 32)
+//   pg_wgrad_kernel  C[a][b] = sum_m A[a][m] B[b][m] over millions of rows:
+//                    one 32x32 output tile per wave, 16 rows per MFMA k-step,
+//                    both operands 16-byte loads from the unit-major arrays;
+//                    row-split partials summed in a fixed order (deterministic)
+// dW1 = X^T dH1, dW2 = H1^T dH2, dW3 = H2^T g_y, db = the same with a ones row.
+// Anchor: the controller chooses "the cheapest and cleanest number of pods and
+// node types that still meet the SLO" (CS218_Project_Proposal.pdf p.1) and the
+// dashboards plot cost / carbon / SLO trade-offs (p.5). SEMANTICS 5.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kparams.h"
+
+namespace ccka {
+
+namespace {
+
+typedef mlp_bf16x8 bf16x8;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) z[k] = 0.f;
+  return z;
+}
+
+// registers 8s..8s+7 -> bf16 (round to nearest even), then ReLU on the bits
+// (as mlp.hip's relu_pack: the forward's exact H1 / H2 operands)
+typedef uint32_t u32x4_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 relu_pack(const f32x16& a, int s) {
+  u32x4_ o;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const bf16x2v b = __builtin_convertvector((f32x2){a[8 * s + 2 * w], a[8 * s + 2 * w + 1]}, bf16x2v);
+    const short2v v = __builtin_elementwise_max(__builtin_bit_cast(short2v, b), (short2v){0, 0});
+    o[w] = __builtin_bit_cast(uint32_t, v);
+  }
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// registers 8s..8s+7 -> bf16, zeroed where the activation h is 0 (ReLU'(h) = 0),
+// whole dwords at a time (each half masked by a 32-bit test of h's half)
+__device__ __forceinline__ bf16x8 mask_pack(const f32x16& a, int s, const bf16x8& h) {
+  const u32x4_ hv = __builtin_bit_cast(u32x4_, h);
+  u32x4_ o;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const bf16x2v b = __builtin_convertvector((f32x2){a[8 * s + 2 * w], a[8 * s + 2 * w + 1]}, bf16x2v);
+    const uint32_t m = ((hv[w] & 0xFFFFu) != 0u ? 0x0000FFFFu : 0u) | ((hv[w] >> 16) != 0u ? 0xFFFF0000u : 0u);
+    o[w] = __builtin_bit_cast(uint32_t, b) & m;
+  }
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// fragment f (64 lanes x 16 B) of a fragment array through a buffer resource:
+// the lane offset is one VGPR and the fragment offset an SGPR, so no 64-bit
+// address per fragment is kept live across the tile loop
+__device__ __forceinline__ bf16x8 frag(__amdgpu_buffer_rsrc_t r, int lane16, int f) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lane16, f * (WAVE * 16), 0));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frag_rsrc(const mlp_bf16x8* p, int nfrag) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, nfrag * WAVE * 16, 0x00020000);
+}
+
+__device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
+  f32x16 a;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(b + 8 * g + 4 * h);
+    a[4 * g + 0] = v[0];
+    a[4 * g + 1] = v[1];
+    a[4 * g + 2] = v[2];
+    a[4 * g + 3] = v[3];
+  }
+  return a;
+}
+
+// hidden unit of element j of k-step fragment q for lane half h (the
+// accumulator row order the forward chains through, mlp.hip)
+__device__ __forceinline__ int kin(int q, int j, int h) { return 16 * q + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+// one fragment's 8 values of this lane's row into a unit-major [unit][Mpad]
+// array: `col` points at (unit 4h, this row); the unit offsets are wave-uniform
+__device__ __forceinline__ void store_frag(uint16_t* __restrict__ col, int64_t Mpad, int q, const bf16x8& v) {
+  const u32x4_ d = __builtin_bit_cast(u32x4_, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    col[(int64_t)(16 * q + 8 * (j >> 2) + (j & 3)) * Mpad] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+}
+
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                                       uint32_t out[4]) {
+#pragma unroll
+  for (int q = 0; q < 10; ++q) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Stochastic policy step (SEMANTICS 5): p = softmax(y) in binary32 (max
+// subtracted, expf); u = Philox(seed; global id, step) as a 24-bit uniform in
+// [0, 1); the action is the first a with u * sum(p) < p_0 + ... + p_a (the
+// last one if rounding leaves none). Action a maps to the HPA target
+// 40 + 10 (a & 3) % and the carbon weight (a >> 2) $/kgCO2.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) policy_sample_kernel(PgSampleParams q) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q.n) return;
+  const float* y = q.y + i * MLP_OUT;
+  float p[MLP_OUT];
+  float mx = y[0];
+#pragma unroll
+  for (int a = 1; a < MLP_OUT; ++a) mx = fmaxf(mx, y[a]);
+  float sum = 0.f;
+#pragma unroll
+  for (int a = 0; a < MLP_OUT; ++a) {
+    p[a] = expf(y[a] - mx);
+    sum += p[a];
+  }
+  const int64_t g = q.first_id + i;
+  uint32_t u4[4];
+  philox((uint32_t)g, (uint32_t)(g >> 32), (uint32_t)q.t, 0x5A3B1E7u, (uint32_t)q.seed, (uint32_t)(q.seed >> 32), u4);
+  const float u = (float)(u4[0] >> 8) * (1.0f / 16777216.0f) * sum;
+  int act = MLP_OUT - 1;  // the last action when rounding leaves u above every partial sum
+  float acc = 0.f;
+  bool found = false;
+#pragma unroll
+  for (int a = 0; a < MLP_OUT; ++a) {
+    acc += p[a];
+    if (!found && u < acc) { act = a; found = true; }
+  }
+  q.act[i] = (uint8_t)act;
+  q.target[i] = (int16_t)(40 + 10 * (act & 3));
+  q.cw[i] = (double)(act >> 2);
+  if (q.rec_target) {
+    q.rec_target[i] = q.target[i];
+    q.rec_cw[i] = q.cw[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward recompute + backward of one 32-row tile per wave (persistent grid).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
+  constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
+  __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 32];
+  __shared__ bf16x8 s_w2[NB * KS2 * WAVE];  // forward W2 fragments, 128 KiB
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+  const int r = lane & 31, h = lane >> 5;
+  for (int x = tid; x < NB * KS2 * WAVE; x += blockDim.x) s_w2[x] = p.w2f[x];
+  for (int x = tid; x < 2 * MLP_HID + 32; x += blockDim.x) s_b[x] = p.bias[x];
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t r1 = frag_rsrc(p.w1f, NB * KS1), r3 = frag_rsrc(p.w3f, KS2);
+  const __amdgpu_buffer_rsrc_t r2b = frag_rsrc(p.w2b, NB * KS2), r3b = frag_rsrc(p.w3b, NB);
+  const int l16 = lane * 16;
+  const int64_t ntiles = p.Mpad / 32;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / WAVE);
+  for (int64_t tl = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave; tl < ntiles; tl += nw) {
+    const int64_t m = tl * 32 + r;  // this lane's row (state)
+    const bool ok = m < p.M;
+    const int64_t Mp = p.Mpad;
+    const int64_t cb = (int64_t)(4 * h) * Mp + m;  // (unit 4h, row m) of a unit-major array
+    // ---- X^T fragments (B operand of layer 1), stored for dW1 ----
+    bf16x8 xf[KS1];
+    {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(p.x + (ok ? m : 0) * MLP_IN + 8 * h);
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) {
+        const bf16x8 v = src[2 * s];
+        xf[s] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const u32x4_ d = __builtin_bit_cast(u32x4_, xf[s]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p.xT[(int64_t)(16 * s + 8 * h + j) * Mp + m] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+    }
+    // ---- layer 1: H1^T = relu(bf16(W1^T X^T + b1)) ----
+    bf16x8 h1[KS2];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      f32x16 c = bias_tile(s_b + 32 * n, h);
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) c = mfma(frag(r1, l16, n * KS1 + s), xf[s], c);
+      h1[2 * n] = relu_pack(c, 0);
+      h1[2 * n + 1] = relu_pack(c, 1);
+      store_frag(p.h1T + cb, Mp, 2 * n, h1[2 * n]);
+      store_frag(p.h1T + cb, Mp, 2 * n + 1, h1[2 * n + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- layer 2: H2^T = relu(bf16(W2^T H1^T + b2)); layer 3: Y^T = W3^T H2^T + b3 ----
+    bf16x8 h2[KS2];
+    f32x16 yv = bias_tile(s_b + 2 * MLP_HID, h);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      f32x16 c = bias_tile(s_b + MLP_HID + 32 * n, h);
+#pragma unroll
+      for (int kk = 0; kk < KS2; ++kk) c = mfma(s_w2[(n * KS2 + kk) * WAVE + lane], h1[kk], c);
+      h2[2 * n] = relu_pack(c, 0);
+      h2[2 * n + 1] = relu_pack(c, 1);
+      store_frag(p.h2T + cb, Mp, 2 * n, h2[2 * n]);
+      store_frag(p.h2T + cb, Mp, 2 * n + 1, h2[2 * n + 1]);
+      yv = mfma(frag(r3, l16, 2 * n), h2[2 * n], yv);
+      yv = mfma(frag(r3, l16, 2 * n + 1), h2[2 * n + 1], yv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- g_y = c (e_a - softmax(y)): logits 4h..4h+3 of row m in registers 0..3 ----
+    const float cf = ok ? p.coef[m % p.n_scen] : 0.f;
+    const int act = ok ? (int)p.act[m] : -1;
+    float mx = fmaxf(fmaxf(yv[0], yv[1]), fmaxf(yv[2], yv[3]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float e[4], se = 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      e[a] = expf(yv[a] - mx);
+      se += e[a];
+    }
+    se += __shfl_xor(se, 32);
+    float gy[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) gy[a] = cf * ((4 * h + a == act ? 1.f : 0.f) - e[a] / se);
+    // B operand of dH2^T = W3 g_y^T (k = action, padded to 16): half 0 holds
+    // actions 0..7 of its row, half 1 zeros
+    float g8[8];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const float o = __shfl_xor(gy[a], 32);
+      g8[a] = h == 0 ? gy[a] : 0.f;
+      g8[4 + a] = h == 0 ? o : 0.f;
+    }
+    u32x4_ gw;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      gw[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){g8[2 * w], g8[2 * w + 1]}, bf16x2v));
+    const bf16x8 gyf = __builtin_bit_cast(bf16x8, gw);
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p.gyT[(int64_t)j * Mp + m] = (uint16_t)(gw[j >> 1] >> (16 * (j & 1)));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- dH2^T = (W3 g_y^T) masked by H2 > 0 (H2 dies here) ----
+    bf16x8 dh2[KS2];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const f32x16 c = mfma(frag(r3b, l16, n), gyf, zero16());
+      dh2[2 * n] = mask_pack(c, 0, h2[2 * n]);
+      dh2[2 * n + 1] = mask_pack(c, 1, h2[2 * n + 1]);
+      store_frag(p.dh2T + cb, Mp, 2 * n, dh2[2 * n]);
+      store_frag(p.dh2T + cb, Mp, 2 * n + 1, dh2[2 * n + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- dH1^T = (W2 dH2^T) masked by H1 > 0, one 32-row block at a time ----
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      f32x16 c = zero16();
+#pragma unroll
+      for (int kk = 0; kk < KS2; ++kk) c = mfma(frag(r2b, l16, n * KS2 + kk), dh2[kk], c);
+      store_frag(p.dh1T + cb, Mp, 2 * n, mask_pack(c, 0, h1[2 * n]));
+      store_frag(p.dh1T + cb, Mp, 2 * n + 1, mask_pack(c, 1, h1[2 * n + 1]));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C[a][b] = sum_m A[a][m] B[b][m] (A: [KA][Mpad], B: [KB][Mpad] bf16,
+// unit-major; rows beyond KA / KB read as zero). Grid: (32x32 output tiles) x
+// (row splits); each wave accumulates one tile over its rows 16 at a time and
+// writes fp32 partials [split][KA][KB]; pg_reduce_kernel sums the splits in
+// order.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) pg_wgrad_kernel(WgradParams q) {
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int tb = (q.KB + 31) / 32;
+  const int tile = blockIdx.x % (((q.KA + 31) / 32) * tb), split = blockIdx.x / (((q.KA + 31) / 32) * tb);
+  const int a0 = tile / tb * 32, b0 = tile % tb * 32;
+  const int64_t chunk = (q.Mpad / 16 + q.splits - 1) / q.splits * 16;
+  const int64_t m0 = (int64_t)split * chunk, m1 = min(m0 + chunk, q.Mpad);
+  const bool va = a0 + r < q.KA, vb = b0 + r < q.KB;
+  const bf16x8* pa = reinterpret_cast<const bf16x8*>(q.A + (int64_t)(va ? a0 + r : 0) * q.Mpad + 8 * h);
+  const bf16x8* pb = reinterpret_cast<const bf16x8*>(q.B + (int64_t)(vb ? b0 + r : 0) * q.Mpad + 8 * h);
+  const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  f32x16 c = zero16();
+  int64_t m = m0;
+  for (; m + 64 <= m1; m += 64) {  // four k-steps in flight
+    bf16x8 x[4], y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = va ? pa[(m + 16 * k) / 8] : z;
+      y[k] = vb ? pb[(m + 16 * k) / 8] : z;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c = mfma(x[k], y[k], c);
+  }
+  for (; m < m1; m += 16) c = mfma(va ? pa[m / 8] : z, vb ? pb[m / 8] : z, c);
+  // accumulator register k: row a0 + (k&3) + 8(k>>2) + 4h, column b0 + r
+  float* out = q.part + (int64_t)split * q.KA * q.KB;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int a = a0 + (k & 3) + 8 * (k >> 2) + 4 * h, b = b0 + r;
+    if (a < q.KA && b < q.KB) out[(int64_t)a * q.KB + b] = c[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) pg_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                        int64_t n, int splits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
+  out[i] = s;
+}
+
+__global__ void __launch_bounds__(256) pg_fill_kernel(uint16_t* __restrict__ x, int64_t n, int64_t valid, uint16_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = i < valid ? v : (uint16_t)0;
+}
+
+hipError_t launch_policy_sample(const PgSampleParams& q, hipStream_t s) {
+  hipLaunchKernelGGL(policy_sample_kernel, dim3((unsigned)((q.n + 255) / 256)), dim3(256), 0, s, q);
+  return hipGetLastError();
+}
+
+hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s) {
+  hipLaunchKernelGGL(pg_rows_kernel, dim3((unsigned)cus), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_pg_wgrad(const WgradParams& q, float* out, hipStream_t s) {
+  const int tiles = ((q.KA + 31) / 32) * ((q.KB + 31) / 32);
+  hipLaunchKernelGGL(pg_wgrad_kernel, dim3((unsigned)(tiles * q.splits)), dim3(64), 0, s, q);
+  const int64_t n = (int64_t)q.KA * q.KB;
+  hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q.part, out, n, q.splits);
+  return hipGetLastError();
+}
+
+hipError_t launch_pg_fill(uint16_t* x, int64_t n, int64_t valid, uint16_t v, hipStream_t s) {
+  hipLaunchKernelGGL(pg_fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n, valid, v);
+  return hipGetLastError();
+}
+
+}  // namespace ccka

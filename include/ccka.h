@@ -406,6 +406,48 @@ int ccka_policy_rollout(ccka_ctx* ctx, int32_t trajectory, int32_t record);
 /* The recorded actions: target [T][N] int16 (%), cw [T][N] double ($/kg). */
 int ccka_get_policy_actions(ccka_ctx* ctx, int16_t* target, double* cw, int64_t count);
 
+/* ---- differentiable control (config 5) -------------------------------- */
+/* The closed loop with a stochastic policy: at every step each scenario samples
+ * an action bin a from softmax(y) (y = the MLP's 8 outputs; Philox keyed by
+ * seed, global id and step), a -> HPA target 40 + 10*(a & 3) % and Karpenter
+ * carbon weight (a >> 2) $/kgCO2 (SEMANTICS 5). The objective of scenario i is
+ * J_i = cost_i [$] + w_carbon * gCO2_i [kg] + w_slo * SLO-minutes_i, and
+ * ccka_policy_grad returns the score-function (likelihood-ratio) estimate
+ *   dE[J]/dW = (1/N) sum_i (J_i - b) sum_t d log pi(a_it | x_it) / dW,
+ * b = mean J when baseline != 0 (else 0): the MLP backward over all N*T
+ * (step, scenario) rows on bf16 MFMA with fp32 accumulation. Proposal anchor:
+ * the controller picks "the cheapest and cleanest" pods / node types that meet
+ * the SLO (CS218_Project_Proposal.pdf p.1); cost/carbon/SLO trade-offs (p.5). */
+typedef struct ccka_pg_params {
+  uint64_t seed;        /* Philox key of the action sampling */
+  double w_carbon;      /* $ per kgCO2 in the objective (>= 0) */
+  double w_slo;         /* $ per SLO-violation minute (>= 0) */
+  int32_t baseline;     /* 1: advantages J - mean(J) */
+  int32_t _pad;
+} ccka_pg_params;
+/* Gradient outputs: caller-owned fp32 host arrays in the layouts of
+ * ccka_mlp_set_weights (w1 [64][256], b1 [256], w2 [256][256], b2 [256],
+ * w3 [256][8], b3 [8]); NULL members are skipped. */
+typedef struct ccka_mlp_grads {
+  float* w1;
+  float* b1;
+  float* w2;
+  float* b2;
+  float* w3;
+  float* b3;
+} ccka_mlp_grads;
+/* One stochastic closed-loop rollout (world, scenarios, load and weights as
+ * ccka_policy_rollout; results / actions read back the same way) and the
+ * gradient of E[J]; *objective_mean (nullable) = mean J of the batch. */
+int ccka_policy_grad(ccka_ctx* ctx, const ccka_pg_params* params, ccka_mlp_grads* out, double* objective_mean);
+/* The sampled action bins [T][N] and the per-scenario factors (J_i - b) / N of
+ * the last ccka_policy_grad (count = T*N). */
+int ccka_get_policy_samples(ccka_ctx* ctx, uint8_t* actions, float* coef, int64_t count);
+/* The MLP backward alone on m given rows: x [m][64] bf16, action bins [m] (< 8),
+ * coef [m]: the gradient of sum_m coef[m] * log softmax(policy(x_m))[a_m]. */
+int ccka_mlp_backward(ccka_ctx* ctx, const uint16_t* x, const uint8_t* actions, const float* coef, int64_t m,
+                      ccka_mlp_grads* out);
+
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------- */
 /* Fill a 128-byte RCCL unique id (rank 0 only; distribute it out of band). */
 int ccka_comm_unique_id(uint8_t* id128);

@@ -139,6 +139,23 @@ def rollout_policy(spec, scen, load, act_target, act_cw, traj=False, threads=1, 
     return arrays, tr, ft
 
 
+def policy_uniform(seed, gids, t):
+    """The stochastic policy's uniform draw of SEMANTICS 5 (the device's
+    policy_sample_kernel): Philox-4x32-10 with counter (id lo, id hi, t,
+    0x5A3B1E7) and key (seed lo, seed hi), top 24 bits of word 0 / 2^24."""
+    L = lib()
+    fn = L.ccka_oracle_philox
+    fn.argtypes = [C.c_uint32] * 6 + [C.POINTER(C.c_uint32)]
+    out = (C.c_uint32 * 4)()
+    u = np.empty(len(gids), np.float64)
+    for k, g in enumerate(gids):
+        g = int(g)
+        fn(g & 0xFFFFFFFF, (g >> 32) & 0xFFFFFFFF, t & 0xFFFFFFFF, 0x5A3B1E7, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF,
+           out)
+        u[k] = (out[0] >> 8) / 16777216.0
+    return u
+
+
 def policy_act(y):
     """The action mapping of SEMANTICS 5 in numpy (fp32, round half to even)."""
     y = np.asarray(y, np.float32)

@@ -26,7 +26,7 @@ for arg in sys.argv[1:]:
                                                     os.path.join(CSRC, src)])))
 for name, out, obj, p in procs:
     assert p.wait() == 0, name
-    others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "sweep.o", "mlp.o", "ccka_abi.o")]
+    others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "sweep.o", "mlp.o", "pg.o", "ccka_abi.o")]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     os.path.join(out, "libccka.so"), obj, *others, "-L/opt/rocm/lib", "-lrccl",
                     "-Wl,-rpath,/opt/rocm/lib"], check=True)
