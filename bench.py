@@ -298,7 +298,7 @@ def main():
         if rank == 0:
             cbw = copy_bandwidth(eng)
             out["roofline"]["copy_gbs"] = cbw
-            out["roofline"]["copy_kernel"] = "copy16_kernel: 2 GiB dwordx4 nontemporal streaming copy, median of 5"
+            out["roofline"]["copy_kernel"] = "copy16_kernel: 2 GiB dwordx4 nontemporal copy, one element per thread, median of 5 (tools/probe/copyprobe.hip)"
             out["roofline"]["frac_of_copy"] = achieved / cbw
         if rank == 0 and world == 1 and not args.no_cpu:
             out["cpu_baseline"], out["parity"], out["parity_detail"] = cpu_baseline(

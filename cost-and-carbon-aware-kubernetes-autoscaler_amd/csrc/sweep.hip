@@ -133,28 +133,24 @@ hipError_t launch_pareto_union(const ccka_grid_stats* gathered, const int64_t* c
 
 // ---------------------------------------------------------------------------
 // Copy ceiling (bench.py's roofline denominator beside the 8 TB/s peak): a
-// plain streaming device copy, 16 bytes per lane per access (dwordx4), eight
-// accesses in flight per lane, nontemporal on both sides, grid sized to fill
-// every CU several times over. Profiling aid, not part of the rollout.
+// plain streaming device copy, 16 bytes per lane (dwordx4), one element per
+// thread with the grid covering the buffer, nontemporal on both sides. The
+// fastest of the variants tools/probe/copyprobe.hip measured on MI355X (6.5
+// TB/s read + write; grid-stride loops with 4-8 accesses in flight per lane:
+// 4.4-4.8 TB/s). Profiling aid, not part of the rollout.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) copy16_kernel(const int4* __restrict__ in, int4* __restrict__ out, int64_t n) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 7 * stride < n; i += 8 * stride) {
-    i32x4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load((const i32x4*)(in + i + k * stride));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(v[k], (i32x4*)(out + i + k * stride));
-  }
-  for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load((const i32x4*)(in + i)),
-                                                         (i32x4*)(out + i));
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load((const i32x4*)(in + i)), (i32x4*)(out + i));
 }
 
 hipError_t launch_copy16(const void* in, void* out, int64_t bytes, int cus, hipStream_t s) {
+  (void)cus;
   const int64_t n = bytes / 16;
-  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)(cus * 8)), dim3(256), 0, s, (const int4*)in, (int4*)out, n);
+  const int64_t grid = (n + 255) / 256;
+  if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)grid), dim3(256), 0, s, (const int4*)in, (int4*)out, n);
   return hipGetLastError();
 }
 
