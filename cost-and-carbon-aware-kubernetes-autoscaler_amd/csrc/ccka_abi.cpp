@@ -567,7 +567,7 @@ static bool rules_ok(const ccka_hpa_rules& r) {
   if (r.stab_window_s < 0 || r.stab_window_s > CCKA_HPA_MAX_WINDOW_S) return false;
   for (int i = 0; i < r.n_policies; ++i) {
     const ccka_hpa_policy& p = r.policies[i];
-    if ((p.type != CCKA_HPA_PODS && p.type != CCKA_HPA_PERCENT) || p.value < 0 || p.period_s < 0 ||
+    if ((p.type != CCKA_HPA_PODS && p.type != CCKA_HPA_PERCENT) || p.value < 0 || p.period_s < 1 ||
         p.period_s > CCKA_HPA_MAX_PERIOD_S)
       return false;
   }
@@ -1067,11 +1067,6 @@ int ccka_rollout(ccka_ctx* c, int32_t trajectory) {
 static int mlp_alloc(ccka_ctx* c, int64_t n);
 
 // ---- closed-loop learned control policy (config 5) ----
-// state words per scenario of the general kernel's persistence block (the
-// order of state_io in rollout.hip)
-static int64_t state_words(int dmax, int nmax) {
-  return (int64_t)dmax * (5 + 2 * CCKA_HIST) + 5 * CCKA_MAX_POOLS + (int64_t)nmax * (6 + dmax) + 36;
-}
 
 // The closed loop (SEMANTICS 5). pg == nullptr: the deterministic policy
 // (policy_act_kernel); otherwise each step samples an action bin from

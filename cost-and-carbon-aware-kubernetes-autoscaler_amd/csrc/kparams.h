@@ -15,6 +15,14 @@ struct DetailDev {
   int64_t base_e_hour;
 };
 
+// Words per scenario of the general kernel's persisted state block (the
+// closed loop): the st_xfer sequence of state_io in rollout.hip, one row per
+// 32-bit value and two per 64-bit value. Host (allocation) and kernel (a
+// check folded away at compile time when the sequence matches) both use it.
+__host__ __device__ constexpr int64_t state_words(int dmax, int nmax) {
+  return (int64_t)dmax * (5 + 2 * CCKA_HIST) + 5 * CCKA_MAX_POOLS + (int64_t)nmax * (6 + dmax) + 36;
+}
+
 struct KParams {
   const ccka_world* w;  // device copy (pools, deployments, scalars)
   const ccka_itype* types;
@@ -206,6 +214,7 @@ struct D1Params {
   int32_t drift_on;                  // 1: Karpenter drift (SEMANTICS 3.G0) acts
   int32_t replace;                   // 1: replacement consolidation offers (SEMANTICS 3.G2)
   const int2* table2;                // [R][24][NZI][3][JT] cheapest offering by price (the G2 offer rule)
+  int32_t lds_tab;                   // set by launch_rollout_d1: price tiles, ci and J staged in LDS
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)

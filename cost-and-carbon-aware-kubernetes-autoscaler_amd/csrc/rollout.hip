@@ -686,6 +686,10 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
     st_xfer(hash, st, k, sN, i, save);
     st_xfer(hpos, st, k, sN, i, save);
     st_xfer(hour, st, k, sN, i, save);
+    // k is a compile-time constant here (every loop above is unrolled): the
+    // trap is folded away while the sequence and state_words() agree, and
+    // stops the kernel before a lane writes past its rows if they ever differ
+    if (k != state_words(DMAX, MAXN)) __builtin_trap();
   };
   const int t0 = p.t0, t1 = p.t1;
   if (p.state && p.state_load) {

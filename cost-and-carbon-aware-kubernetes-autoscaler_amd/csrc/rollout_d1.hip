@@ -340,6 +340,20 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #ifndef D1_LAZYH_V
 #define D1_LAZYH_V 0
 #endif
+// price tiles, carbon intensity and J from an LDS copy when they fit (the
+// event step's hour-change reads then wait for no older vector-memory
+// operation: every global load does, the trajectory stores and trace DMAs
+// included)
+#ifndef D1_LDST_V
+#define D1_LDST_V 1
+#endif
+// top-of-iteration wait: with the lean quiet path every iteration issues
+// exactly D1_S record stores after its refill DMAs, and vector-memory
+// operations complete in issue order, so vmcnt(D1_VMN + D1_S) still retires
+// every row but the D1_VMN youngest while leaving the records in flight
+#ifndef D1_WAITS_V
+#define D1_WAITS_V 0
+#endif
 constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
 constexpr int D1_K = D1_K_V;      // event cadence (iterations)
 constexpr int D1_VMN = D1_VMN_V;  // rows in flight (vmcnt bound; <= 63)
@@ -352,6 +366,22 @@ constexpr int D1_BACK = D1_LEAN_V == 2 ? CCKA_HIST : 0;
 static_assert(D1_VMN + 4 * D1_S + D1_BACK <= D1_RB && D1_RB - D1_S - D1_BACK - D1_VMN >= 2 * D1_S,
               "ring too small for the DMA lead");
 constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
+// packed ring rows: a row holds the wave's lpw scenarios (4 lpw bytes), so
+// the same D1_RING_BYTES hold 4096 / lpw rows (83 at 49 lanes instead of 64)
+// and the lanes may drift further apart before the slowest one blocks the
+// refill (the row count is then a runtime value: rows by modulo, not mask)
+#ifndef D1_PACK_V
+#define D1_PACK_V 0
+#endif
+// x mod n for 0 <= x < 2^17, n <= 4096, rn = 1/(float)n: the f32 quotient is
+// within one of the truth, one correction on each side makes it exact
+__device__ __forceinline__ int d1_mod(int x, int n, float rn) {
+  const int q = (int)((float)x * rn);
+  int r = x - q * n;
+  r += r < 0 ? n : 0;
+  r -= r >= n ? n : 0;
+  return r;
+}
 
 // streaming hint on the trace rows (build variant)
 #ifndef D1_NTL_V
@@ -385,10 +415,56 @@ __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row)
       : "v"(src), "s"(lds_row)
       : "memory");
 }
+template <bool LEAN>
 __device__ __forceinline__ void d1_wait_rows() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN) : "memory");
+  if constexpr (LEAN && D1_WAITS_V) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN + D1_S) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN) : "memory");
 }
 __device__ __forceinline__ void d1_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Argmin-table reads of the event step through the scalar data cache: a
+// vector load would wait for every older vector-memory operation of the wave
+// (the last iteration's trajectory stores and trace DMAs: they complete in
+// issue order), a scalar load only for older scalar ones. The active lanes'
+// addresses are taken four at a time (v_readlane), loaded with s_load_dwordx2
+// and handed back to their lanes.
+#ifndef D1_SLD_V
+#define D1_SLD_V 1
+#endif
+#define CONST_AS __attribute__((address_space(4)))
+__device__ __forceinline__ int2 d1_tload(const GLOBAL_AS int2* ptr) {
+  if constexpr (!D1_SLD_V) {
+    const uint64_t v = *(const GLOBAL_AS uint64_t*)ptr;
+    return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
+  } else {
+    const uint64_t a = (uint64_t)ptr;
+    const int alo = (int)(uint32_t)a, ahi = (int)(uint32_t)(a >> 32);
+    const int me = (int)(threadIdx.x & (WAVE - 1));
+    uint64_t m = __ballot(1);
+    int ox = 0, oy = 0;
+    while (m) {
+      int l[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        l[k] = m ? __ffsll((long long)m) - 1 : l[0];
+        m &= m - 1;  // (0 stays 0)
+      }
+      uint64_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t ak = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(alo, l[k]) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane(ahi, l[k]) << 32;
+        v[k] = *(const CONST_AS uint64_t*)ak;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ox = me == l[k] ? (int)(uint32_t)v[k] : ox;
+        oy = me == l[k] ? (int)(uint32_t)(v[k] >> 32) : oy;
+      }
+    }
+    return make_int2(ox, oy);
+  }
+}
 
 // logical block of dispatch block b among n (a bijection; 8 XCDs)
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
@@ -406,6 +482,20 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   for (int x = threadIdx.x; x < p.K; x += blockDim.x) {
     const long long idle = p.acc[x * 3 + 0];
     s_acc[x] = make_int4((int)(idle & 0xffffffffLL), (int)(idle >> 32), (int)p.acc[x * 3 + 1], (int)p.acc[x * 3 + 2]);
+  }
+  // LDS copies of the price tiles [R][24][K][Z][2], ci [R][24] and J
+  // [R][24][NZI][3] after the rings (launch_rollout_d1 sets lds_tab when they fit)
+  const bool ldt = D1_LDST_V && p.lds_tab;
+  const uint32_t tab_off = ((uint32_t)p.K * 16u + 255u) / 256u * 256u + (blockDim.x / WAVE) * (uint32_t)D1_RING_BYTES;
+  const int n_pr = p.R * 24 * p.K * p.Z * 2;
+  const int n_pr8 = (n_pr + 1) & ~1;
+  int* const s_price = reinterpret_cast<int*>(reinterpret_cast<char*>(s_acc) + tab_off);
+  double* const s_ci = reinterpret_cast<double*>(s_price + n_pr8);
+  int* const s_jtab = reinterpret_cast<int*>(s_ci + p.R * 24);
+  if (ldt) {
+    for (int x = threadIdx.x; x < n_pr; x += blockDim.x) s_price[x] = p.price[x];
+    for (int x = threadIdx.x; x < p.R * 24; x += blockDim.x) s_ci[x] = p.ci_gpwmin[x];
+    for (int x = threadIdx.x; x < p.R * 24 * p.NZI * 3; x += blockDim.x) s_jtab[x] = p.jtab[x];
   }
   __syncthreads();
   // lanes-per-wave mapping: wave w owns scenarios [w*lpw, (w+1)*lpw)
@@ -593,7 +683,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
     for (int q = 0; q < MAXP; ++q) {
       const uint32_t cm = pcm[q] & capsel;
-      pJ[q] = (q < NP && cm && pzi[q] >= 0) ? jtab[((int64_t)rh * NZI + pzi[q]) * 3 + (cm - 1)] : 0;
+      const int64_t ji = ((int64_t)rh * NZI + pzi[q]) * 3 + (cm - 1);
+      pJ[q] = (q < NP && cm && pzi[q] >= 0) ? (ldt ? s_jtab[ji] : jtab[ji]) : 0;
     }
   };
 
@@ -775,11 +866,30 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // LDS byte address (the low word of the generic address of an LDS object)
   const uint32_t ring_lds = (uint32_t)(uintptr_t)s_acc + ring_off;
   const int* const ring = reinterpret_cast<const int*>(reinterpret_cast<const char*>(s_acc) + ring_off);
-  int tf = 0;  // trace rows issued (wave-uniform)
+  // ring geometry (wave-uniform): rbn rows of rsw lanes; row of step x = x mod rbn
+  const int rsw = D1_PACK_V ? opq(p.lpw) : WAVE;
+  const int rbn = D1_PACK_V ? min(D1_RING_BYTES / (4 * rsw), 4096) : D1_RB;
+  const float rrbn = D1_PACK_V ? 1.0f / (float)rbn : 0.f;
+  auto rrow = [&](int x) { return D1_PACK_V ? d1_mod(x, rbn, rrbn) : (x & (D1_RB - 1)); };
+  // ring index of (row r, this lane)
+  auto ridx = [&](int r) { return r * rsw + lane; };
+  // row r + q (0 <= q < rbn) wrapped
+  auto rnext = [&](int r, int q) { return D1_PACK_V ? (r + q >= rbn ? r + q - rbn : r + q) : ((r + q) & (D1_RB - 1)); };
+  int tf = 0;   // trace rows issued (wave-uniform)
+  int tfr = 0;  // tf mod rbn (wave-uniform)
   const int32_t* lpf = lp;  // this lane's sample of row tf
+  auto tf_adv = [&]() {
+    ++tf;
+    ++tfr;
+    if (tfr == rbn) tfr = 0;
+    lpf += lsl;
+  };
   {
     const int n0 = min(T, D1_VMN + 4 * D1_S);
-    for (; tf < n0; ++tf, lpf += lsl) d1_dma_row(lpf, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4));
+    while (tf < n0) {
+      d1_dma_row(lpf, (uint32_t)__builtin_amdgcn_readfirstlane((int)(ring_lds + (uint32_t)tfr * (uint32_t)(rsw * 4))));
+      tf_adv();
+    }
     d1_wait_all();
   }
   int t_rdy = tf;  // rows < t_rdy have landed (wave-uniform)
@@ -806,7 +916,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   for (int it = 0;; ++it) {
     const bool live = t < T;
     if (__ballot(live) == 0) break;  // wave-uniform
-    d1_wait_rows();
+    d1_wait_rows<BDEF && D1_LEAN_V == 2>();
     t_rdy = max(t_rdy, tf - D1_VMN);
     // ---- event steps of the stalled lanes: every D1_K iterations, or when no
     // lane stepped quietly in the last one. They run before this iteration's
@@ -828,7 +938,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       HpaOut hp{};
       if (ev) {
         stall = false;
-        L = ring[(t & (D1_RB - 1)) * WAVE + lane];
+        const int tr = rrow(t);
+        L = ring[ridx(tr)];
         if constexpr (BDEF && D1_LEAN_V == 2) {
           // the down-window records of the quiet steps [tq, t), oldest first,
           // from their trace rows (the ring keeps >= 8 rows behind every lane)
@@ -857,7 +968,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             bool anylow = false;
 #pragma unroll
             for (int j = 0; j < CCKA_HIST; ++j) {
-              us[j] = min(ring[((t - 1 - j) & (D1_RB - 1)) * WAVE + lane], q_rcap);
+              us[j] = min(ring[ridx(rnext(tr, rbn - 1 - j))], q_rcap);
               rv[j] = q_met ? cur16 : (int)0x8000;
               anylow |= (j < kq) & q_met & (us[j] < q_pge);
             }
@@ -1028,16 +1139,19 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // here, after the phases that do not read them, since every load
         // waits for all older memory operations (this iteration's records) ----
         if (hchg) {
-          const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
-          ci_min = ci_gpwmin[rh];
-          base_price = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
+          const int64_t toff = (int64_t)rh * K * Z * 2;
+          const GLOBAL_AS int32_t* tile = price + toff;
+          const int* stile = s_price + toff;
+          ci_min = ldt ? s_ci[rh] : ci_gpwmin[rh];
+          base_price = (long long)base_nodes * (ldt ? stile[(base_type * Z) * 2 + 1] : tile[(base_type * Z) * 2 + 1]);
           burn = 0;
           // every slot's price in flight at once (unused slots read entry 0)
           int np[MAXN];
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
             const uint32_t x = sinfo[n];
-            np[n] = tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
+            const int e = ((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u);
+            np[n] = ldt ? stile[e] : tile[e];
           }
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
@@ -1069,7 +1183,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 const int slot = __ffs((int)fm) - 1;
                 fm &= fm - 1;
                 const int k = min(J, pd);
-                const int2 e = *(const int2*)(row + k);  // never empty: k <= J
+                const int2 e = d1_tload(row + k);  // never empty: k <= J
                 const int info = e.y, price = e.x;
                 const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
                 const int rs = t + delay;
@@ -1272,7 +1386,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                   for (int qq = 0; qq < MAXP; ++qq)
                     if (qq == q) { J = pJ[qq]; zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
                   if (cmq && zq >= 0 && need <= J)
-                    e = *(const int2*)(table + ((((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * NW + wi) * JT + need);
+                    e = d1_tload(table + ((((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * NW + wi) * JT + need);
                 }
                 if (e.y >= 0 && need > 0) {
                   const int info = e.y, price = e.x;
@@ -1441,7 +1555,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                     if (qq == q) { zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
                   int2 e = make_int2(0, -1);
                   if (!(pdb_member && bp > allowed) && cmq && zq >= 0)
-                    e = *(const int2*)(table2 + (((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * JT + bp);
+                    e = d1_tload(table2 + (((int64_t)rh * NZI + zq) * 3 + (cmq - 1)) * JT + bp);
                   if (e.y < 0 || e.x >= bpr) {  // PDB, no offer or not strictly cheaper
                     c2 &= ~(1u << best);
                     continue;
@@ -1588,7 +1702,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           // upp = floor(usage / ready) = trunc((usage + 0.5) / ready) in binary32 for
           // usage < 2^20 (the quotient stays 0.5/ready clear of an integer; the
           // correctly rounded reciprocal and the single fma rounding are far inside that)
-          q_rbp = rpods > 0 ? 1.0f / (float)rpods : 0.f;
+          // (v_rcp_f32, <= 1 ulp: with the fma rounding the estimate is within
+          // 0.19/ready of (usage + 0.5)/ready, which lies >= 0.5/ready from an integer)
+          q_rbp = rpods > 0 ? __builtin_amdgcn_rcpf((float)rpods) : 0.f;
           q_hbp = 0.5f * q_rbp;
           // no node saturates while upp <= q_usat (pods*upp < alloc on every node)
           q_usat = Rmax > 0.f ? (int)fminf(0.9999f * __builtin_amdgcn_rcpf(Rmax), 1073741824.0f) - 1 : 0x7fffffff;
@@ -1677,10 +1793,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     // what they overwrite; issued after the event steps, whose own loads
     // wait for every older vector-memory operation ----
     if (tf < T) {
-      if (__ballot(t < T && t < tf + D1_S - D1_RB + D1_BACK) == 0) {
+      if (__ballot(t < T && t < tf + D1_S - rbn + D1_BACK) == 0) {
         const int n1 = min(T, tf + D1_S);
-        for (; tf < n1; ++tf)
-          d1_dma_row(lpf, ring_lds + (uint32_t)(tf & (D1_RB - 1)) * (WAVE * 4)), lpf += lsl;
+        while (tf < n1) {
+          d1_dma_row(lpf, (uint32_t)__builtin_amdgcn_readfirstlane((int)(ring_lds + (uint32_t)tfr * (uint32_t)(rsw * 4))));
+          tf_adv();
+        }
         if (tf == T) {  // no younger DMA will retire the last rows
           d1_wait_all();
           t_rdy = T;
@@ -1689,8 +1807,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
     bool adv = false;
     if (!pf_ok) {  // a row landed after the prefetch (or the lane left an event step)
+      const int tr = rrow(t);
 #pragma unroll
-      for (int q = 0; q < D1_S; ++q) Lpf[q] = ring[((t + q) & (D1_RB - 1)) * WAVE + lane];
+      for (int q = 0; q < D1_S; ++q) Lpf[q] = ring[ridx(rnext(tr, q))];
     }
 
     D1_STAMP(8);
@@ -1818,8 +1937,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     // this lane's next samples (the LDS latency hides under the loop tail);
     // rows that have not landed yet are read again at the top
     pf_ok = t + (D1_S - 1) < t_rdy;
+    {
+      const int tr = rrow(t);
 #pragma unroll
-    for (int q = 0; q < D1_S; ++q) Lpf[q] = ring[((t + q) & (D1_RB - 1)) * WAVE + lane];
+      for (int q = 0; q < D1_S; ++q) Lpf[q] = ring[ridx(rnext(tr, q))];
+    }
     D1_STAMP(8);
   }
   d1_wait_all();  // no LDS-DMA may outlive the wave
@@ -1904,26 +2026,35 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const int B = 256;
   const int64_t waves = (p.N + p.lpw - 1) / p.lpw;
   const unsigned grid = (unsigned)((waves + B / WAVE - 1) / (B / WAVE));
-  const size_t lds = ((size_t)p.K * sizeof(int4) + 255) / 256 * 256 + (size_t)(B / WAVE) * D1_RING_BYTES;
+  size_t lds = ((size_t)p.K * sizeof(int4) + 255) / 256 * 256 + (size_t)(B / WAVE) * D1_RING_BYTES;
+  // price tiles, ci and J in LDS when two blocks per CU still fit (<= 80 KB each)
+  const size_t npr = (size_t)p.R * 24 * p.K * p.Z * 2;
+  const size_t tabB = ((npr + 1) & ~(size_t)1) * 4 + (size_t)p.R * 24 * 8 + (size_t)p.R * 24 * p.NZI * 3 * 4;
+  D1Params q = p;
+  q.lds_tab = 0;
+  if (D1_LDST_V && lds + tabB <= 80 * 1024) {
+    q.lds_tab = 1;
+    lds += tabB;
+  }
   // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
   if (p.drift) {  // drift (SEMANTICS 3.G0): 8 slots, <= 2 pools (d1_disrupt_ok)
-    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true>), dim3(grid), dim3(B), lds, s, p);
-    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true>), dim3(grid), dim3(B), lds, s, p);
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true>), dim3(grid), dim3(B), lds, s, q);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.stamps) {
-    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, p);
-    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, false>), dim3(grid), dim3(B), lds, s, p);
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, q);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.maxn <= 8 && p.NP <= 2 && p.occ == 3) {
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 3, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 3, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.maxn <= 8 && p.NP <= 2) {
-    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true>), dim3(grid), dim3(B), lds, s, p);
-    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false>), dim3(grid), dim3(B), lds, s, p);
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true>), dim3(grid), dim3(B), lds, s, q);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.maxn <= 8) {
-    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false, 2, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false, 2, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.NP <= 2) {
-    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false, 1, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 2, false, 1, false>), dim3(grid), dim3(B), lds, s, q);
   } else {
-    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false, 1, false>), dim3(grid), dim3(B), lds, s, p);
+    hipLaunchKernelGGL((rollout_d1_kernel<16, 4, false, 1, false>), dim3(grid), dim3(B), lds, s, q);
   }
   return hipGetLastError();
 }

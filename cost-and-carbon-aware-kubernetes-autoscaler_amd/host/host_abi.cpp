@@ -1,4 +1,5 @@
 // host_abi.cpp — C ABI of libccka_host.so (include/ccka_host.h).
+#include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <exception>
@@ -10,6 +11,42 @@
 #include "policy.h"
 
 using namespace ccka::host;
+
+// printf-style append of any length (no fixed line buffer: long names are
+// never truncated)
+static void appendf(std::string& o, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static void appendf(std::string& o, const char* fmt, ...) {
+  char b[256];
+  va_list ap;
+  va_start(ap, fmt);
+  const int n = std::vsnprintf(b, sizeof b, fmt, ap);
+  va_end(ap);
+  if (n < 0) return;
+  if ((size_t)n < sizeof b) {
+    o.append(b, (size_t)n);
+    return;
+  }
+  const size_t at = o.size();
+  o.resize(at + (size_t)n + 1);
+  va_start(ap, fmt);
+  std::vsnprintf(&o[at], (size_t)n + 1, fmt, ap);
+  va_end(ap);
+  o.resize(at + (size_t)n);
+}
+
+// Prometheus text exposition label value: backslash, double quote and line
+// feed escaped (exposition format 0.0.4)
+static std::string prom_esc(const std::string& v) {
+  std::string r;
+  r.reserve(v.size());
+  for (char ch : v) {
+    if (ch == '\\') r += "\\\\";
+    else if (ch == '"') r += "\\\"";
+    else if (ch == '\n') r += "\\n";
+    else r += ch;
+  }
+  return r;
+}
 
 struct ccka_host {
   PolicyEnv env;
@@ -185,42 +222,35 @@ int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r, 
       return i < (int)v.size() && !v[(size_t)i].empty() ? v[(size_t)i] : std::string(dflt);
     };
     std::string s;
-    char b[512];
     const int T = w->n_steps;
     s += "# ccka summary: node pools, cost and carbon (demo_41_observe_cost_nodes)\n";
-    std::snprintf(b, sizeof b, "horizon: %d steps x %d s   pools: %d   deployments: %d   catalog: %d types\n\n",
+    appendf(s, "horizon: %d steps x %d s   pools: %d   deployments: %d   catalog: %d types\n\n",
                   T, CCKA_STEP_SECONDS, w->n_pools, w->n_deploy, w->n_types);
-    s += b;
     // ---- NodePools: demo_20_offpeak_observe.sh:9-20 views at the last step
     const bool peak = traj ? (traj[T - 1].flags & 1u) != 0 : peak_at(w, T - 1);
-    std::snprintf(b, sizeof b, "[Observe] Disruption settings (last step, %s profile)\n", peak ? "peak" : "off-peak");
-    s += b;
+    appendf(s, "[Observe] Disruption settings (last step, %s profile)\n", peak ? "peak" : "off-peak");
     for (int q = 0; q < w->n_pools; ++q) {
       const ccka_pool_patch e = pool_at_end(w, q, peak);
-      std::snprintf(b, sizeof b, "== %s ==\nconsolidationPolicy=%s  consolidateAfter=%s\n", pool_name(q).c_str(),
+      appendf(s, "== %s ==\nconsolidationPolicy=%s  consolidateAfter=%s\n", pool_name(q).c_str(),
                     e.policy == CCKA_WHEN_EMPTY ? "WhenEmpty" : "WhenEmptyOrUnderutilized",
                     duration_text(e.consolidate_after_s).c_str());
-      s += b;
       s += "topology.kubernetes.io/zone=In: ";
       for (int z = 0; z < w->n_zones; ++z)
         if (e.zone_mask >> z & 1u) s += M.zone_prefix + (char)('a' + z) + " ";
       s += "\nkarpenter.sh/capacity-type=In: ";
       if (e.cap_mask & CCKA_CAP_SPOT) s += "spot ";
       if (e.cap_mask & CCKA_CAP_OD) s += "on-demand ";
-      std::snprintf(b, sizeof b, "\nlabels: autoscale.strategy=%s carbon.simulated=%s   budget: nodes %d%%",
+      appendf(s, "\nlabels: autoscale.strategy=%s carbon.simulated=%s   budget: nodes %d%%",
                     label_or(M.pool_strategy, q, "<none>").c_str(), label_or(M.pool_carbon, q, "<none>").c_str(),
                     w->pools[q].budget_pct);
-      s += b;
       if (w->pools[q].limit_cpu_m >= 0) {
-        std::snprintf(b, sizeof b, "   limits: cpu %dm", w->pools[q].limit_cpu_m);
-        s += b;
+        appendf(s, "   limits: cpu %dm", w->pools[q].limit_cpu_m);
       }
       s += "\n";
     }
     // ---- Deployments: demo_30_burst_observe.sh:10-11 custom columns
     s += "\n# Summary of deployments (last step)\n";
-    std::snprintf(b, sizeof b, "%-24s %-7s %-8s %s\n", "NAME", "READY", "DESIRED", "CAPACITY");
-    s += b;
+    appendf(s, "%-24s %-7s %-8s %s\n", "NAME", "READY", "DESIRED", "CAPACITY");
     for (int d = 0; d < w->n_deploy; ++d) {
       if (w->deploy[d].scaler == CCKA_SCALER_KEDA_TRIGGER) continue;  // a trigger, not a Deployment
       const std::string nm = d < (int)M.deploy_names.size() ? M.deploy_names[(size_t)d] : "?";
@@ -230,36 +260,31 @@ int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r, 
         if (det->ready[d] > 0) ready = std::to_string(det->ready[d]);
         desired = std::to_string(det->desired[d]);
       }
-      std::snprintf(b, sizeof b, "%-24s %-7s %-8s %s\n", nm.c_str(), ready.c_str(), desired.c_str(),
+      appendf(s, "%-24s %-7s %-8s %s\n", nm.c_str(), ready.c_str(), desired.c_str(),
                     label_or(M.deploy_capacity, d, "<none>").c_str());
-      s += b;
     }
     if (!det) s += "(* manifest replicas: run with the detail breakdown for the rollout's values)\n";
     if (traj) {
       const ccka_traj_rec& last = traj[T - 1];
-      std::snprintf(b, sizeof b, "pods: desired=%d pending=%d   nodes: spot=%u on-demand=%u\n", last.replicas,
+      appendf(s, "pods: desired=%d pending=%d   nodes: spot=%u on-demand=%u\n", last.replicas,
                     last.pending, last.nodes_spot, last.nodes_od);
-      s += b;
     }
     // ---- nodes
     const uint32_t lc = r->last_choice ? r->last_choice[0] : 0xFFFFFFFFu;
     s += "\n# Nodes\n";
-    std::snprintf(b, sizeof b, "  node-minutes spot=%d on-demand=%d   peak nodes=%d   launches=%d deletions=%d\n",
+    appendf(s, "  node-minutes spot=%d on-demand=%d   peak nodes=%d   launches=%d deletions=%d\n",
                   r->node_min_spot[0], r->node_min_od[0], r->peak_nodes[0], r->launches[0], r->deletions[0]);
-    s += b;
     if (lc != 0xFFFFFFFFu) {
       const int k = (int)(lc & 0xFFF), z = (int)((lc >> 12) & 3), c = (int)((lc >> 14) & 3), q = (int)(lc >> 16);
-      std::snprintf(b, sizeof b, "  last launch: %s zone=%s%c capacity=%s pool=%s\n",
+      appendf(s, "  last launch: %s zone=%s%c capacity=%s pool=%s\n",
                     k < (int)h->tables.names.size() ? h->tables.names[(size_t)k].c_str() : "?", M.zone_prefix.c_str(),
                     'a' + z, c == 0 ? "spot" : "on-demand", pool_name(q).c_str());
-      s += b;
     }
     // ---- cost and carbon by pool and by carbon.simulated group
     if (det) {
       s += "\n# Cost and carbon by node pool\n";
-      std::snprintf(b, sizeof b, "%-24s %-8s %10s %10s %15s %8s %11s %12s %12s\n", "NODEPOOL", "CARBON", "NODEMIN-S",
+      appendf(s, "%-24s %-8s %10s %10s %15s %8s %11s %12s %12s\n", "NODEPOOL", "CARBON", "NODEMIN-S",
                     "NODEMIN-OD", "NODES(END/PEAK)", "LAUNCHES", "COST($)", "ENERGY(kWh)", "gCO2");
-      s += b;
       std::vector<std::pair<std::string, double>> gcost, gkwh, gco2;
       auto add = [](std::vector<std::pair<std::string, double>>& v, const std::string& k, double x) {
         for (auto& e : v)
@@ -269,39 +294,33 @@ int ccka_host_summary(ccka_host* h, const ccka_world* w, const ccka_results* r, 
       for (int q = 0; q < w->n_pools; ++q) {
         const std::string grp = label_or(M.pool_carbon, q, "<none>");
         const double usd = (double)det->pool_cost_uphmin[q] / 6e7, kwh = (double)det->pool_energy_nwmin[q] * 1e-9 / 6e4;
-        std::snprintf(b, sizeof b, "%-24s %-8s %10d %10d %15s %8d %11.4f %12.4f %12.2f\n", pool_name(q).c_str(),
+        appendf(s, "%-24s %-8s %10d %10d %15s %8d %11.4f %12.4f %12.2f\n", pool_name(q).c_str(),
                       grp.c_str(), det->pool_node_min_spot[q], det->pool_node_min_od[q],
                       (std::to_string(det->pool_final_nodes[q]) + "/" + std::to_string(det->pool_peak_nodes[q])).c_str(),
                       det->pool_launches[q], usd, kwh, det->pool_gco2[q]);
-        s += b;
         add(gcost, grp, usd);
         add(gkwh, grp, kwh);
         add(gco2, grp, det->pool_gco2[q]);
       }
       const double busd = (double)det->base_cost_uphmin / 6e7, bkwh = (double)det->base_energy_nwmin * 1e-9 / 6e4;
-      std::snprintf(b, sizeof b, "%-24s %-8s %10s %10d %15s %8s %11.4f %12.4f %12.2f\n", "(base managed nodes)", "<none>",
+      appendf(s, "%-24s %-8s %10s %10d %15s %8s %11.4f %12.4f %12.2f\n", "(base managed nodes)", "<none>",
                     "-", w->base_nodes * T, (std::to_string(w->base_nodes) + "/" + std::to_string(w->base_nodes)).c_str(),
                     "-", busd, bkwh, det->base_gco2);
-      s += b;
       add(gcost, "<none>", busd);
       add(gkwh, "<none>", bkwh);
       add(gco2, "<none>", det->base_gco2);
       s += "\n# By carbon.simulated group (demo_10_setup_configure.sh:61-62 labels)\n";
-      std::snprintf(b, sizeof b, "%-10s %11s %12s %12s\n", "GROUP", "COST($)", "ENERGY(kWh)", "gCO2");
-      s += b;
+      appendf(s, "%-10s %11s %12s %12s\n", "GROUP", "COST($)", "ENERGY(kWh)", "gCO2");
       for (size_t g = 0; g < gcost.size(); ++g) {
-        std::snprintf(b, sizeof b, "%-10s %11.4f %12.4f %12.2f\n", gcost[g].first.c_str(), gcost[g].second,
+        appendf(s, "%-10s %11.4f %12.4f %12.2f\n", gcost[g].first.c_str(), gcost[g].second,
                       gkwh[g].second, gco2[g].second);
-        s += b;
       }
     }
     s += "\n# Cost and carbon (run total)\n";
-    std::snprintf(b, sizeof b, "  cost=$%.4f   energy=%.4f kWh   carbon=%.2f gCO2\n", (double)r->cost_uphmin[0] / 6e7,
+    appendf(s, "  cost=$%.4f   energy=%.4f kWh   carbon=%.2f gCO2\n", (double)r->cost_uphmin[0] / 6e7,
                   r->energy_wmin[0] / 6e4, r->gco2[0]);
-    s += b;
-    std::snprintf(b, sizeof b, "  SLO violation minutes=%d   pending pod-minutes=%lld\n", r->slo_minutes[0],
+    appendf(s, "  SLO violation minutes=%d   pending pod-minutes=%lld\n", r->slo_minutes[0],
                   (long long)r->pending_pod_minutes[0]);
-    s += b;
     return put(h, s, out, cap);
   });
 }
@@ -318,35 +337,31 @@ int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const cc
     const int start = ((w->start_minute % 1440) + 1440) % 1440;
     auto rec = [&](int t, int64_t s) -> const ccka_traj_rec& { return traj[(int64_t)t * traj_n + s0 + s]; };
     std::string o;
-    char b[512];
     if (format == CCKA_EXPORT_CSV) {
       o.reserve((size_t)(n * T * 40 + 128));
       o += "scenario,step,minute,replicas,pending,nodes_spot,nodes_od,last_type,flags\n";
       for (int64_t s = 0; s < n; ++s)
         for (int t = 0; t < T; ++t) {
           const ccka_traj_rec& x = rec(t, s);
-          std::snprintf(b, sizeof b, "%lld,%d,%d,%d,%d,%u,%u,%u,%u\n", (long long)(first_id + s0 + s), t,
+          appendf(o, "%lld,%d,%d,%d,%d,%u,%u,%u,%u\n", (long long)(first_id + s0 + s), t,
                         (start + t) % 1440, x.replicas, x.pending, x.nodes_spot, x.nodes_od, x.last_type, x.flags);
-          o += b;
         }
     } else {
       o.reserve((size_t)(n * T * 7 * 110 + 4096));
-      const std::string ns = h->env.ns;
-      const std::string dep = w->n_deploy == 1 && !h->meta.deploy_names.empty() ? h->meta.deploy_names[0]
+      const std::string ns = prom_esc(h->env.ns);
+      const std::string dep = w->n_deploy == 1 && !h->meta.deploy_names.empty() ? prom_esc(h->meta.deploy_names[0])
                               : w->n_deploy == 1                                 ? std::string("deployment-0")
                                                                                  : std::string("all");
       auto family = [&](const char* name, const char* type, const char* help) {
-        std::snprintf(b, sizeof b, "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
-        o += b;
+        appendf(o, "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
       };
       auto ts = [&](int t) { return (long long)(start_unix_ms + (int64_t)t * CCKA_STEP_SECONDS * 1000); };
       auto dep_series = [&](const char* name, const char* type, const char* help, auto value) {
         family(name, type, help);
         for (int64_t s = 0; s < n; ++s)
           for (int t = 0; t < T; ++t) {
-            std::snprintf(b, sizeof b, "%s{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %lld %lld\n", name,
+            appendf(o, "%s{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %lld %lld\n", name,
                           ns.c_str(), dep.c_str(), (long long)(first_id + s0 + s), (long long)value(rec(t, s)), ts(t));
-            o += b;
           }
       };
       dep_series("kube_deployment_spec_replicas", "gauge", "Number of desired pods for a deployment.",
@@ -362,34 +377,30 @@ int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const cc
         for (int64_t s = 0; s < n; ++s)
           for (int t = 0; t < T; ++t) {
             const ccka_traj_rec& x = rec(t, s);
-            std::snprintf(b, sizeof b, "ccka_nodes{scenario=\"%lld\",capacity_type=\"%s\"} %u %lld\n",
+            appendf(o, "ccka_nodes{scenario=\"%lld\",capacity_type=\"%s\"} %u %lld\n",
                           (long long)(first_id + s0 + s), c == 0 ? "spot" : "on-demand",
                           c == 0 ? (unsigned)x.nodes_spot : (unsigned)x.nodes_od, ts(t));
-            o += b;
           }
       family("ccka_policy_profile", "gauge", "1 while the peak NodePool profile is applied, 0 off-peak.");
       for (int64_t s = 0; s < n; ++s)
         for (int t = 0; t < T; ++t) {
-          std::snprintf(b, sizeof b, "ccka_policy_profile{scenario=\"%lld\"} %u %lld\n", (long long)(first_id + s0 + s),
+          appendf(o, "ccka_policy_profile{scenario=\"%lld\"} %u %lld\n", (long long)(first_id + s0 + s),
                         rec(t, s).flags & 1u, ts(t));
-          o += b;
         }
       family("ccka_step_event", "gauge", "1 when the step launched a node, deleted a node or violated the SLO.");
       static const char* ev[3] = {"launch", "deletion", "slo_violation"};
       for (int e = 0; e < 3; ++e)
         for (int64_t s = 0; s < n; ++s)
           for (int t = 0; t < T; ++t) {
-            std::snprintf(b, sizeof b, "ccka_step_event{scenario=\"%lld\",event=\"%s\"} %u %lld\n",
+            appendf(o, "ccka_step_event{scenario=\"%lld\",event=\"%s\"} %u %lld\n",
                           (long long)(first_id + s0 + s), ev[e], (rec(t, s).flags >> (e + 1)) & 1u, ts(t));
-            o += b;
           }
       // run totals at the last step
       auto total = [&](const char* name, const char* type, const char* help, const char* extra, auto value) {
         family(name, type, help);
         for (int64_t s = 0; s < n; ++s) {
-          std::snprintf(b, sizeof b, "%s{scenario=\"%lld\"%s} %.17g %lld\n", name, (long long)(first_id + s0 + s), extra,
+          appendf(o, "%s{scenario=\"%lld\"%s} %.17g %lld\n", name, (long long)(first_id + s0 + s), extra,
                         (double)value(s0 + s), ts(T - 1));
-          o += b;
         }
       };
       if (r->cost_uphmin)
@@ -411,10 +422,9 @@ int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const cc
         family("ccka_node_minutes_total", "counter", "Karpenter node-minutes of the run by capacity type.");
         for (int c = 0; c < 2; ++c)
           for (int64_t s = 0; s < n; ++s) {
-            std::snprintf(b, sizeof b, "ccka_node_minutes_total{scenario=\"%lld\",capacity_type=\"%s\"} %d %lld\n",
+            appendf(o, "ccka_node_minutes_total{scenario=\"%lld\",capacity_type=\"%s\"} %d %lld\n",
                           (long long)(first_id + s0 + s), c == 0 ? "spot" : "on-demand",
                           c == 0 ? r->node_min_spot[s0 + s] : r->node_min_od[s0 + s], ts(T - 1));
-            o += b;
           }
       }
       if (r->launches)
@@ -431,11 +441,10 @@ int ccka_host_export(ccka_host* h, int32_t format, const ccka_world* w, const cc
           long long pod_min = 0;
           for (int t = 0; t < T; ++t) pod_min += (long long)rec(t, s).replicas - rec(t, s).pending;
           if (pod_min <= 0) continue;
-          std::snprintf(b, sizeof b,
+          appendf(o,
                         "ccka_pod_cost_dollars_per_hour{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %.17g %lld\n",
                         ns.c_str(), dep.c_str(), (long long)(first_id + s0 + s),
                         ((double)r->cost_uphmin[s0 + s] / 6e7) / ((double)pod_min / 60.0), ts(T - 1));
-          o += b;
         }
       }
     }
@@ -458,24 +467,21 @@ int ccka_host_export_detail(ccka_host* h, const ccka_world* w, const ccka_detail
     const WorldMeta& M = h->meta;
     const long long ts = (long long)(start_unix_ms + (int64_t)(w->n_steps - 1) * CCKA_STEP_SECONDS * 1000);
     std::string o;
-    char b[640];
     auto family = [&](const char* name, const char* type, const char* help) {
-      std::snprintf(b, sizeof b, "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
-      o += b;
+      appendf(o, "# HELP %s %s\n# TYPE %s %s\n", name, help, name, type);
     };
-    auto lab = [&](const std::vector<std::string>& v, int q) { return q < (int)v.size() ? v[(size_t)q] : std::string(); };
+    auto lab = [&](const std::vector<std::string>& v, int q) { return q < (int)v.size() ? prom_esc(v[(size_t)q]) : std::string(); };
     // one sample per (scenario, group); group P = the base managed node group
     auto pool_series = [&](const char* name, const char* type, const char* help, auto value) {
       family(name, type, help);
       for (int64_t s = 0; s < n; ++s)
         for (int q = 0; q <= w->n_pools; ++q) {
           const bool base = q == w->n_pools;
-          const std::string np = base ? std::string("base-managed") : (q < (int)M.pool_names.size() ? M.pool_names[(size_t)q] : "?");
-          std::snprintf(b, sizeof b,
+          const std::string np = base ? std::string("base-managed") : (q < (int)M.pool_names.size() ? prom_esc(M.pool_names[(size_t)q]) : "?");
+          appendf(o,
                         "%s{scenario=\"%lld\",nodepool=\"%s\",carbon_simulated=\"%s\",autoscale_strategy=\"%s\"} %.17g %lld\n",
                         name, (long long)(first_id + s), np.c_str(), base ? "" : lab(M.pool_carbon, q).c_str(),
                         base ? "" : lab(M.pool_strategy, q).c_str(), value(det[s], q, base), ts);
-          o += b;
         }
     };
     pool_series("ccka_nodepool_cost_dollars_total", "counter", "Node cost of the run per NodePool (base: managed node group).",
@@ -494,22 +500,20 @@ int ccka_host_export_detail(ccka_host* h, const ccka_world* w, const ccka_detail
     for (int64_t s = 0; s < n; ++s)
       for (int q = 0; q < w->n_pools; ++q)
         for (int c = 0; c < 2; ++c) {
-          std::snprintf(b, sizeof b,
+          appendf(o,
                         "ccka_nodepool_node_minutes_total{scenario=\"%lld\",nodepool=\"%s\",carbon_simulated=\"%s\","
                         "capacity_type=\"%s\"} %d %lld\n",
-                        (long long)(first_id + s), q < (int)M.pool_names.size() ? M.pool_names[(size_t)q].c_str() : "?",
+                        (long long)(first_id + s), q < (int)M.pool_names.size() ? prom_esc(M.pool_names[(size_t)q]).c_str() : "?",
                         lab(M.pool_carbon, q).c_str(), c == 0 ? "spot" : "on-demand",
                         c == 0 ? det[s].pool_node_min_spot[q] : det[s].pool_node_min_od[q], ts);
-          o += b;
         }
     family("kube_deployment_status_replicas_ready", "gauge", "The number of ready replicas per deployment (last step).");
     for (int64_t s = 0; s < n; ++s)
       for (int d = 0; d < w->n_deploy; ++d) {
         if (w->deploy[d].scaler == CCKA_SCALER_KEDA_TRIGGER) continue;
-        std::snprintf(b, sizeof b, "kube_deployment_status_replicas_ready{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %d %lld\n",
-                      h->env.ns.c_str(), d < (int)M.deploy_names.size() ? M.deploy_names[(size_t)d].c_str() : "?",
+        appendf(o, "kube_deployment_status_replicas_ready{namespace=\"%s\",deployment=\"%s\",scenario=\"%lld\"} %d %lld\n",
+                      prom_esc(h->env.ns).c_str(), d < (int)M.deploy_names.size() ? prom_esc(M.deploy_names[(size_t)d]).c_str() : "?",
                       (long long)(first_id + s), det[s].ready[d], ts);
-        o += b;
       }
     if (needed) *needed = (int64_t)o.size() + 1;
     if (!out || (int64_t)o.size() + 1 > cap) {

@@ -65,6 +65,29 @@ void ManifestStore::patch(const std::string& kind, const std::string& name, cons
   *o = std::move(copy);
 }
 
+// apimachinery validation (IsQualifiedName / IsValidLabelValue): a name is
+// at most 63 characters of [A-Za-z0-9._-], alphanumeric at both ends; a key
+// is an optional DNS-subdomain prefix (<= 253 characters, lowercase
+// alphanumerics, '-' and '.') and '/' before such a name; a value is empty or
+// such a name
+static bool label_name_ok(const std::string& v) {
+  if (v.empty() || v.size() > 63) return false;
+  auto alnum = [](char c) { return std::isalnum((unsigned char)c) != 0; };
+  if (!alnum(v.front()) || !alnum(v.back())) return false;
+  for (char c : v)
+    if (!alnum(c) && c != '-' && c != '_' && c != '.') return false;
+  return true;
+}
+static bool label_key_ok(const std::string& k) {
+  const size_t sl = k.find('/');
+  if (sl == std::string::npos) return label_name_ok(k);
+  const std::string pre = k.substr(0, sl), nm = k.substr(sl + 1);
+  if (pre.empty() || pre.size() > 253 || !label_name_ok(nm)) return false;
+  for (char c : pre)
+    if (!(std::islower((unsigned char)c) || std::isdigit((unsigned char)c) || c == '-' || c == '.')) return false;
+  return std::isalnum((unsigned char)pre.front()) && std::isalnum((unsigned char)pre.back());
+}
+
 void ManifestStore::label(const std::string& kind, const std::string& name, const std::string& labels,
                           bool overwrite) {
   Value* o = find(kind, name);
@@ -93,6 +116,9 @@ void ManifestStore::label(const std::string& kind, const std::string& name, cons
     }
     const std::string key = tok.substr(0, eq), val = tok.substr(eq + 1);
     if (key.empty()) throw ParseError("error: invalid label spec: " + tok);
+    if (!label_key_ok(key) || !(val.empty() || label_name_ok(val)))
+      throw ParseError("error: invalid label spec: " + tok +
+                       " (keys and values: <= 63 characters of [A-Za-z0-9._-], alphanumeric at both ends)");
     if (const Value* cur = ls->get(key); cur && cur->as_string() != val && !overwrite)
       throw ParseError("error: '" + key + "' already has a value (" + cur->as_string() +
                        "), and --overwrite is false");

@@ -401,7 +401,12 @@ int ccka_mlp_get_actions(ccka_ctx* ctx, float* y, int64_t n);
  * Karpenter carbon weight rint(16 y1)/16 clamped to 0..4 $/kgCO2 (they replace
  * the scenarios' target_util_pct / carbon_weight overrides). World, scenarios
  * and load as ccka_rollout; results / trajectory / totals / detail read back
- * the same way. record != 0 keeps the actions of every step. */
+ * the same way. record != 0 keeps the actions of every step.
+ * The loop runs on the context's MLP state and action buffers: afterwards
+ * the MLP state count is N and the states are the last step's features (as
+ * if ccka_mlp_set_states had been called with them), so a later
+ * ccka_mlp_forward evaluates those; states set before are replaced.
+ * ccka_policy_grad does the same. */
 int ccka_policy_rollout(ccka_ctx* ctx, int32_t trajectory, int32_t record);
 /* The recorded actions: target [T][N] int16 (%), cw [T][N] double ($/kg). */
 int ccka_get_policy_actions(ccka_ctx* ctx, int16_t* target, double* cw, int64_t count);

@@ -118,3 +118,33 @@ def test_export_detail_series():
     ready = [ln for ln in prom.splitlines() if ln.startswith("kube_deployment_status_replicas_ready{")]
     assert len(ready) == 12 and 'scenario="7"' in ready[0]
     assert sum(int(ln.split()[1]) for ln in ready) == int(det["ready"][0, :12].sum())
+
+
+def test_label_syntax_validated_like_kubectl():
+    """apimachinery label rules (IsQualifiedName / IsValidLabelValue): kubectl
+    rejects these before they reach the object."""
+    h = _demo_host(labels=False)
+    for bad in ("carbon.simulated=" + "x" * 64, "carbon.simulated=-low", "carbon.simulated=lo_",
+                'carbon.simulated=a"b', "b@d=1", "Example.com/x=1", "/x=1", "x/=1"):
+        with pytest.raises(abi.CckaError, match="invalid label spec"):
+            h.label("NodePool", "spot-preferred", bad)
+    h.label("NodePool", "spot-preferred", "example.com/strategy=cost carbon.simulated=")
+    got = json.loads(h.get_json("NodePool", "spot-preferred"))["metadata"]["labels"]
+    assert got == {"example.com/strategy": "cost", "carbon.simulated": ""}
+
+
+def test_export_detail_long_labels_not_truncated():
+    """A 63-character label value (the kubectl maximum) reaches every
+    Prometheus line whole; no line is cut short or loses its newline."""
+    h = _demo_host(labels=False)
+    v = "c" + "a" * 61 + "z"
+    h.label("NodePool", "spot-preferred", f"carbon.simulated={v} autoscale.strategy={v}")
+    w, r, res, traj, det, _keep = _run(h, steps=120)
+    prom = h.export_detail(w, det)
+    assert prom.endswith("\n")
+    lines = [ln for ln in prom.splitlines() if ln.startswith("ccka_nodepool_cost_dollars_total{")]
+    spot = [ln for ln in lines if 'nodepool="spot-preferred"' in ln]
+    assert spot and f'carbon_simulated="{v}",autoscale_strategy="{v}"}}' in spot[0]
+    for ln in prom.splitlines():
+        if ln and not ln.startswith("#"):
+            assert re.fullmatch(r'[a-z_]+\{[^}]*\} \S+ \d+', ln), ln
