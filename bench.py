@@ -55,6 +55,12 @@ def main():
                     help="configs 2-4 with Karpenter drift at the zone switch (SEMANTICS 3.G0; general kernel)")
     ap.add_argument("--replace", action="store_true",
                     help="configs 2-4 with single-node replacement consolidation (SEMANTICS 3.G2)")
+    ap.add_argument("--multi", action="store_true",
+                    help="configs 2-4 with multi-node consolidation (SEMANTICS 3.G3, Karpenter's default for "
+                         "WhenEmptyOrUnderutilized pools)")
+    ap.add_argument("--hpa-sync", type=int, default=0, choices=[0, 10, 15, 20, 30, 60],
+                    help="HPA decision period in seconds (Kubernetes default 15: four decisions per one-minute "
+                         "step; 0 = one per step)")
     ap.add_argument("--spawn", action="store_true",
                     help="run the ranks as fresh child processes even at --gpus 1 (the launcher path)")
     args = ap.parse_args()
@@ -157,6 +163,8 @@ def main():
             traj = (args.mode or "summary") == "trajectory"
         spec.drift = int(args.drift)
         spec.replace = int(args.replace)
+        spec.multi = int(args.multi)
+        spec.hpa_sync_s = args.hpa_sync
         eng.set_world(spec)
         eng.set_scenarios(sc)
         eng.gen_load(gen)
@@ -275,20 +283,24 @@ def main():
             "scaling": "strong" if cfg == 3 else "weak", "vs_baseline": None, "dtype": "int32+int64+f64",
             "data": "synthetic (on-device Philox load traces, seed 20251205)",
             "config": {"workload": workloads[cfg] + (" + Karpenter drift at the zone switch" if args.drift else "")
-                       + (" + replacement consolidation" if args.replace else ""),
+                       + (" + replacement consolidation" if args.replace else "")
+                       + (" + multi-node consolidation" if args.multi else "")
+                       + (f" + HPA sync every {args.hpa_sync} s" if args.hpa_sync not in (0, 60) else ""),
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
                        "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None if args.drift or args.replace else measured_traffic(cfg, traj, N, T),
+                         "traffic": None if args.drift or args.replace or args.multi or args.hpa_sync not in (0, 60)
+                         else measured_traffic(cfg, traj, N, T),
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},
             # the kernel is issue-bound, not HBM-bound: its measured issue-side
             # utilisation (profiled) and the measured copy ceiling
             # (profiled on the single-deployment kernel only)
-            "issue": profiled_issue(cfg) if engine_id == 2 else None,
+            "issue": profiled_issue(cfg) if engine_id == 2 and not (args.drift or args.replace or args.multi or
+                                                                   args.hpa_sync not in (0, 60)) else None,
             "totals": {"cost_usd": totals.cost_uphmin / 6e7, "energy_kwh": totals.energy_wmin / 6e4,
                        "gco2_kg": totals.gco2 / 1e3, "slo_minutes": totals.slo_minutes,
                        "launches": totals.launches, "deletions": totals.deletions},

@@ -261,6 +261,10 @@ static bool d1_rule_is_default(const D1Rule& r, bool up) {
   return true;
 }
 
+// longest down-stabilisation window the 15 s sync ring holds: 20 records,
+// (W - 1) / 15 <= 20
+constexpr int kD1Sync15MaxWindow = 315;
+
 static int d1_check_world(ccka_ctx* c) {
   const ccka_world& w = c->hw;
   c->d1_world = false;
@@ -271,8 +275,12 @@ static int d1_check_world(ccka_ctx* c) {
   // consolidation are checked per scenario set in d1_prepare (d1_disrupt_ok)
   for (int q = 0; q < w.n_pools; ++q)
     if (w.pools[q].limit_cpu_m >= 0 || w.pools[q].limit_mem_mi >= 0) return CCKA_OK;
-  // one HPA decision per step over the 8-entry register rings
-  if ((w.hpa_sync_s != 0 && w.hpa_sync_s != CCKA_STEP_SECONDS) || !rules_fit_ring(dp.up) || !rules_fit_ring(dp.down))
+  // one HPA decision per step over the 8-entry register rings, or the
+  // Kubernetes default 15 s sync (four per step) with the default behavior
+  // (checked below) over 20-entry rings
+  const bool sync15 = w.hpa_sync_s == 15;
+  if ((w.hpa_sync_s != 0 && w.hpa_sync_s != CCKA_STEP_SECONDS && !sync15) || !rules_fit_ring(dp.up) ||
+      !rules_fit_ring(dp.down))
     return CCKA_OK;
   if (!(dp.tolerance >= 0.0 && dp.tolerance < 1.0) || dp.req_cpu_m < 1 || dp.req_cpu_m > 65535 ||
       dp.limit_cpu_m > 65535 ||
@@ -351,6 +359,8 @@ static int d1_check_world(ccka_ctx* c) {
   p.up = d1_rule(dp.up, true);
   p.dn = d1_rule(dp.down, false);
   p.bdef = d1_rule_is_default(p.up, true) && d1_rule_is_default(p.dn, false);
+  p.nsub = sync15 ? 4 : 1;
+  if (sync15 && (!p.bdef || dp.down.stab_window_s > kD1Sync15MaxWindow)) return CCKA_OK;
   c->d1_world = true;
   return CCKA_OK;
 }
@@ -423,7 +433,8 @@ static int d1_prepare(ccka_ctx* c) {
   c->d1.drift = (drift || replace) ? 1 : 0;  // the DRIFT instantiation carries both
   c->d1.drift_on = drift ? 1 : 0;
   c->d1.replace = replace ? 1 : 0;
-  if (c->sc_dstab_max > CCKA_HIST * CCKA_STEP_SECONDS) return CCKA_OK;  // beyond the register ring
+  // beyond the register ring
+  if (c->sc_dstab_max > (c->d1.nsub == 4 ? kD1Sync15MaxWindow : CCKA_HIST * CCKA_STEP_SECONDS)) return CCKA_OK;
   const size_t n = (size_t)c->N;
   std::vector<double> wl;
   std::vector<uint8_t> wci;

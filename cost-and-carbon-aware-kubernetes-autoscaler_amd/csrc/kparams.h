@@ -215,6 +215,7 @@ struct D1Params {
   int32_t replace;                   // 1: replacement consolidation offers (SEMANTICS 3.G2)
   const int2* table2;                // [R][24][NZI][3][JT] cheapest offering by price (the G2 offer rule)
   int32_t lds_tab;                   // set by launch_rollout_d1: price tiles, ci and J staged in LDS
+  int32_t nsub;                      // HPA decisions per step: 1, or 4 (15 s sync, default behavior)
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)

@@ -216,11 +216,18 @@ __device__ __forceinline__ int wmask(int window_s) {
 
 // packed int16 history rings: entry k (k steps old, 0 = this step) sits in
 // half k&1 of word k>>1
+template <int W = 4>
 __device__ __forceinline__ void ring_push(uint32_t* r, int v) {
-  r[3] = __builtin_amdgcn_alignbit(r[3], r[2], 16);
-  r[2] = __builtin_amdgcn_alignbit(r[2], r[1], 16);
-  r[1] = __builtin_amdgcn_alignbit(r[1], r[0], 16);
+#pragma unroll
+  for (int w = W - 1; w > 0; --w) r[w] = __builtin_amdgcn_alignbit(r[w], r[w - 1], 16);
   r[0] = (r[0] << 16) | ((uint32_t)v & 0xFFFFu);
+}
+// four equal records at once (one step of 15 s decisions): a two-word shift
+template <int W>
+__device__ __forceinline__ void ring_push4(uint32_t* r, int v) {
+#pragma unroll
+  for (int w = W - 1; w > 1; --w) r[w] = r[w - 2];
+  r[1] = r[0] = ((uint32_t)v & 0xFFFFu) * 0x10001u;
 }
 
 typedef short short2v __attribute__((ext_vector_type(2)));
@@ -472,8 +479,13 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
   return x * q + min(x, r) + k;
 }
 
-template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false>
+// NSUB: HPA decisions per step (1, or 4 = the Kubernetes default 15 s sync
+// period, SEMANTICS 3.C sub-steps; upstream default behavior only). The down-
+// stabilisation records then cover 4 decisions per step: HW packed words.
+template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
+  static_assert(NSUB == 1 || (NSUB == 4 && BDEF && D1_LEAN_V == 2 && D1_HELD_V), "15 s sync: lean default path");
+  constexpr int HW = NSUB == 1 ? 4 : 10;  // history words (2 records each)
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   // LDS: per instance type {idle_nw lo, idle_nw hi, dyn_nw_per_m, alloc_cpu_m}
@@ -512,7 +524,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int r = p.region ? (int)p.region[i] : 0;
   const int target = p.target ? (int)p.target[i] : p.target0;
   const int mx = p.maxr ? (int)p.maxr[i] : p.maxr0;
-  const int dnmask = wmask(p.down_stab ? (int)p.down_stab[i] : p.dstab0);
+  const int dwin = p.down_stab ? (int)p.down_stab[i] : p.dstab0;
+  // records inside the down window: entries k < (W - 1) / sync (o_entries)
+  const int nd = NSUB == 1 ? __popc(wmask(dwin)) : (dwin > 15 ? min((dwin - 1) / 15, 2 * HW) : 0);
+  const int dnmask = NSUB == 1 ? wmask(dwin) : 0;
   const int reset_ca = p.reset_ca ? (int)p.reset_ca[i] : p.reset_ca0;
   const int pswitch = p.pswitch ? (int)p.pswitch[i] : p.pswitch0;
   const int wi = p.wci ? (int)p.wci[i] : 0;
@@ -620,13 +635,14 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // recommendations with invalid entries stored as the neutral element of the
   // max (hdn) and of the min (hup), and scale deltas. With the default
   // behavior only the down window reads history (no up window, 15 s periods).
-  uint32_t hdn[4], hup[4], hdel[4] = {0, 0, 0, 0};
-  uint32_t dn16[4];  // this scenario's down-stabilisation window as packed lane masks
+  uint32_t hdn[HW], hup[4], hdel[4] = {0, 0, 0, 0};
+  uint32_t dn16[HW];  // this scenario's down-stabilisation window as packed lane masks
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < 4; ++w) hup[w] = 0x7FFF7FFFu;
+#pragma unroll
+  for (int w = 0; w < HW; ++w) {
     hdn[w] = 0x80008000u;
-    hup[w] = 0x7FFF7FFFu;
-    dn16[w] = ((dnmask >> (2 * w)) & 1 ? 0xFFFFu : 0u) | ((dnmask >> (2 * w + 1)) & 1 ? 0xFFFF0000u : 0u);
+    dn16[w] = (2 * w < nd ? 0xFFFFu : 0u) | (2 * w + 1 < nd ? 0xFFFF0000u : 0u);
   }
   int next_ready = 0x7fffffff, nsp = 0, nod = 0;
   // free pod capacity of the compatible ready slots (kept incrementally)
@@ -653,7 +669,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int q_hold = -0x40000000;     // the down window holds a record >= cur up to this step
   bool q_atmax = false, q_pend = false;  // cur >= maxReplicas, pending pods
   int q_umax = -1;  // largest usage the quiet step evaluates exactly (-1: every step is an event)
-  const int wl = __popc(dnmask);  // down window: the last wl records
+  (void)dnmask;
+  // steps a record >= cur holds the replica count for (every decision of a
+  // later step must see it: (nd - (NSUB - 1)) / NSUB whole steps), and the
+  // steps whose records the event step rebuilds (they reach nd entries back)
+  const int wl = NSUB == 1 ? nd : max(0, (nd - (NSUB - 1)) / NSUB);
+  const int wr = NSUB == 1 ? nd : (nd + NSUB - 1) / NSUB;
   // LEAN 2 quiet step (default behavior): the HPA outcome of a quiet step is a
   // pair of integer compares on the step's usage. Between two event steps the
   // replica count, the ready pods and the node set are constant, so the
@@ -753,7 +774,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       {
         short2v a = as_s2(bfi(dn16[0], hdn[0], 0x80008000u));
 #pragma unroll
-        for (int w = 1; w < 4; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
+        for (int w = 1; w < HW; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
         dnr = max(dnr, max((int)a.x, (int)a.y));
       }
       const int rc = min(max(cur, upr), dnr);
@@ -779,7 +800,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // records clamp to int16 (replicas stay in [0, 32767]; min/max commute with clamping)
   auto hpa_commit = [&](const HpaOut& h, int cur) {
     const int rv = min(max(h.proposal, -D1_REC_SAT - 1), D1_REC_SAT);
-    ring_push(hdn, h.ran ? rv : (int)0x8000);
+    ring_push<HW>(hdn, h.ran ? rv : (int)0x8000);
     if constexpr (!BDEF) {
       ring_push(hup, h.ran ? rv : 0x7FFF);
       ring_push(hdel, (h.hpa_path && h.desired != cur) ? h.desired - cur : 0);
@@ -946,7 +967,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           // and the state they ran with. A record >= cur is stored as cur: the
           // default behavior only ever compares it with a proposal and with cur
           // (<= maxReplicas), so its excess over cur never changes a decision.
-          const int kq = min(t - tq, wl);
+          const int kq = min(t - tq, wr);
           if constexpr (!D1_HELD_V) {
             // every quiet record is cur (or invalid without a metric)
             const int rv = q_met ? min(replicas, D1_REC_SAT) : (int)0x8000;
@@ -1001,7 +1022,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             }
 #pragma unroll
             for (int j = CCKA_HIST - 1; j >= 0; --j)
-              if (j < kq) ring_push(hdn, rv[j]);
+              if (j < kq) {
+                if constexpr (NSUB == 1) ring_push<HW>(hdn, rv[j]);
+                else ring_push4<HW>(hdn, rv[j]);  // the step's NSUB equal records
+              }
           }
         }
         flush(t);
@@ -1084,11 +1108,16 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       D1_STAMP(3);
       if (ev) {
         // ---- C. HPA ----
-        const int cur = replicas;
-        hp = hpa_eval(L, cur, rpods, __builtin_amdgcn_rcpf((float)(rpods * req)),
-                                   __builtin_amdgcn_rcpf((float)(cur * req)));
-        hpa_commit(hp, cur);
-        replicas = hp.desired;
+        // NSUB decisions on the step's metric sample (the ready pods do not
+        // change between them: the ReplicaSet acts after the last)
+#pragma unroll
+        for (int sub = 0; sub < NSUB; ++sub) {
+          const int cur = replicas;
+          hp = hpa_eval(L, cur, rpods, __builtin_amdgcn_rcpf((float)(rpods * req)),
+                        __builtin_amdgcn_rcpf((float)(cur * req)));
+          hpa_commit(hp, cur);
+          replicas = hp.desired;
+        }
 
         // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
         if (placed > replicas) {
@@ -1746,9 +1775,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         if constexpr (BDEF) {  // newest history record >= the new replica count
           int hit = -0x40000000;
 #pragma unroll
-          for (int k = CCKA_HIST - 1; k >= 0; --k) {
+          for (int k = 2 * HW - 1; k >= 0; --k) {
             const int e = (int)(short)(hdn[k >> 1] >> (16 * (k & 1)));
-            hit = e >= replicas ? t - k : hit;
+            hit = e >= replicas ? t - k / NSUB : hit;
           }
           q_hold = replicas <= minr ? 0x3fffffff : hit + wl;
           // LEAN 2 without a metric: no records, nothing to hold
@@ -2038,7 +2067,10 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   }
   // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
-  if (p.drift) {  // drift (SEMANTICS 3.G0): 8 slots, <= 2 pools (d1_disrupt_ok)
+  if (p.nsub == 4) {  // 15 s HPA sync, default behavior (d1_check_world)
+    if (p.drift) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 4>), dim3(grid), dim3(B), lds, s, q);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, false, 4>), dim3(grid), dim3(B), lds, s, q);
+  } else if (p.drift) {  // drift (SEMANTICS 3.G0): 8 slots, <= 2 pools (d1_disrupt_ok)
     if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.stamps) {
