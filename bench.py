@@ -61,6 +61,9 @@ def main():
     ap.add_argument("--hpa-sync", type=int, default=0, choices=[0, 10, 15, 20, 30, 60],
                     help="HPA decision period in seconds (Kubernetes default 15: four decisions per one-minute "
                          "step; 0 = one per step)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="config 5 --mode policy: enqueue the loop's launches directly instead of replaying its "
+                         "captured hipGraph")
     ap.add_argument("--spawn", action="store_true",
                     help="run the ranks as fresh child processes even at --gpus 1 (the launcher path)")
     args = ap.parse_args()
@@ -129,6 +132,9 @@ def main():
         eng.set_scenarios(sc)
         eng.gen_load(configs.trace_gen())
         traj = False
+        fn = eng.lib.ccka_debug_policy_graph
+        fn.argtypes = [C.c_void_p, C.c_int32]
+        eng._chk(fn(eng.ctx, 0 if args.no_graph else 1), "ccka_debug_policy_graph")
 
         def step_fn():
             eng.policy_rollout(trajectory=False)
@@ -227,7 +233,8 @@ def main():
             "data": "synthetic (on-device Philox traces, Xavier-uniform weights seed 11)",
             "config": {"workload": f"config5 closed loop: {N} clusters x {T} steps, every step featurize -> "
                                    "MLP 64->256->256->8 -> HPA target + carbon weight -> rollout step",
-                       "clusters_per_gpu": N, "steps": T, "parallelism": f"data-parallel x{world}"},
+                       "clusters_per_gpu": N, "steps": T, "parallelism": f"data-parallel x{world}",
+                       "launch": "direct" if args.no_graph else "hipGraph (captured loop, replayed)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
                          "kernel": "whole loop (mlp_kernel + policy_act_kernel + rollout_kernel per step)",

@@ -134,6 +134,11 @@ struct ccka_ctx {
   int64_t pol_rec_count = 0;
   bool pol_rec_valid = false;
   bool pol_feat_on = false;
+  // the closed loop's launch sequence captured as one hipGraph, replayed while
+  // its inputs (launch parameters, buffers, sizes) are unchanged
+  hipGraphExec_t pol_graph = nullptr;
+  std::vector<unsigned char> pol_graph_key;
+  bool pol_graph_off = false;  // ccka_debug_policy_graph(0): launch the sequence directly
   uint16_t* d_feat_rec = nullptr;
   int64_t pol_feat_count = 0;
   // differentiable control (ccka_policy_grad / ccka_mlp_backward, pg.hip)
@@ -402,7 +407,7 @@ static bool d1_drift_inert(const ccka_ctx* c) {
 // unless provably inert. Replacement needs an on-demand node in a
 // WhenEmptyOrUnderutilized pool: inert when no pool profile uses that policy
 // or no scenario's nodeSelector admits on-demand; multi-node consolidation
-// needs a WhenEmptyOrUnderutilized pool.
+// needs a WhenEmptyOrUnderutilized pool and a budget of >= 2 nodes.
 static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace) {
   const ccka_world& w = c->hw;
   *drift = !d1_drift_inert(c);
@@ -420,7 +425,16 @@ static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace) {
       *replace = true;
     }
   }
-  if ((w.disrupt_ext & CCKA_DISRUPT_MULTI) && weou) return false;
+  if ((w.disrupt_ext & CCKA_DISRUPT_MULTI) && weou) {
+    // Multi-node consolidation moves >= 2 nodes of a pool in one step: its
+    // firstN search tries prefixes of at most budget - deleted candidates
+    // (SEMANTICS 3.G3). With every pool's disruption budget at <= 1 node for
+    // any node count the world allows (ceil(pct * max_nodes / 100) <= 1: the
+    // reference's 10 % at 8 nodes) there is no prefix to try, so it never acts
+    // and this kernel is exact; larger budgets run on the general kernel.
+    for (int q = 0; q < w.n_pools; ++q)
+      if ((w.pools[q].budget_pct * w.max_nodes + 99) / 100 >= 2) return false;
+  }
   return true;
 }
 
@@ -567,6 +581,7 @@ void ccka_close(ccka_ctx* c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_mid) (void)hipEventDestroy(c->ev_mid);
+  if (c->pol_graph) (void)hipGraphExecDestroy(c->pol_graph);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1166,39 +1181,89 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
                              c->stream));
     return CCKA_OK;
   };
+  PgSampleParams q0{};
+  if (pg) {
+    q0.y = c->d_my;
+    q0.target = c->d_pol_target;
+    q0.cw = c->d_pol_cw;
+    q0.n = N;
+    q0.first_id = c->first_id;
+    q0.seed = pg->seed;
+  }
+  // the whole loop: state initialisation (t = 0, features of step 0), then
+  // per step MLP -> actions -> one rollout step (+ the features kept)
+  auto enqueue = [&]() -> int {
+    k.t0 = 0;
+    k.t1 = 0;
+    k.state_load = 0;
+    HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+    if ((rc = keep_feat(0)) != CCKA_OK) return rc;
+    for (int t = 0; t < T; ++t) {
+      HIPCHK(c, launch_mlp(mp, c->cus, c->stream));
+      if (pg) {
+        PgSampleParams q = q0;
+        q.act = c->d_pg_act + (size_t)t * N;
+        q.rec_target = record ? c->d_rec_target + (size_t)t * N : nullptr;
+        q.rec_cw = record ? c->d_rec_cw + (size_t)t * N : nullptr;
+        q.t = t;
+        HIPCHK(c, launch_policy_sample(q, c->stream));
+      } else {
+        HIPCHK(c, launch_policy_act(c->d_my, c->d_pol_target, c->d_pol_cw,
+                                    record ? c->d_rec_target + (size_t)t * N : nullptr,
+                                    record ? c->d_rec_cw + (size_t)t * N : nullptr, N, c->stream));
+      }
+      k.t0 = t;
+      k.t1 = t + 1;
+      k.state_load = 1;
+      HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+      if ((rc = keep_feat(t + 1)) != CCKA_OK) return rc;
+    }
+    return CCKA_OK;
+  };
+  // graph key: every input of the sequence (parameter blocks by value: their
+  // device pointers and sizes)
+  std::vector<unsigned char> key;
+  auto put = [&](const void* v, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(v);
+    key.insert(key.end(), b, b + n);
+  };
+  {
+    KParams k0 = k;
+    k0.t0 = k0.t1 = k0.state_load = 0;
+    put(&k0, sizeof k0);
+    put(&mp, sizeof mp);
+    put(&q0, sizeof q0);
+    const int64_t misc[10] = {N, T, block, (int64_t)lds, record, feat_on, pg != nullptr, c->cus,
+                              (int64_t)(uintptr_t)c->d_feat_rec, (int64_t)(uintptr_t)c->d_rec_target};
+    put(misc, sizeof misc);
+    const void* ptrs[3] = {c->d_rec_cw, c->d_pg_act, c->stream};
+    put(ptrs, sizeof ptrs);
+  }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
-  // t = 0: initialise the state, features of step 0 (no step runs)
-  k.t0 = 0;
-  k.t1 = 0;
-  k.state_load = 0;
-  HIPCHK(c, launch_rollout(k, block, lds, c->stream));
-  if ((rc = keep_feat(0)) != CCKA_OK) return rc;
-  for (int t = 0; t < T; ++t) {
-    HIPCHK(c, launch_mlp(mp, c->cus, c->stream));
-    if (pg) {
-      PgSampleParams q{};
-      q.y = c->d_my;
-      q.act = c->d_pg_act + (size_t)t * N;
-      q.target = c->d_pol_target;
-      q.cw = c->d_pol_cw;
-      q.rec_target = record ? c->d_rec_target + (size_t)t * N : nullptr;
-      q.rec_cw = record ? c->d_rec_cw + (size_t)t * N : nullptr;
-      q.n = N;
-      q.first_id = c->first_id;
-      q.seed = pg->seed;
-      q.t = t;
-      HIPCHK(c, launch_policy_sample(q, c->stream));
-    } else {
-      HIPCHK(c, launch_policy_act(c->d_my, c->d_pol_target, c->d_pol_cw,
-                                  record ? c->d_rec_target + (size_t)t * N : nullptr,
-                                  record ? c->d_rec_cw + (size_t)t * N : nullptr, N, c->stream));
+  if (c->pol_graph_off) {
+    if ((rc = enqueue()) != CCKA_OK) return rc;
+  } else {
+    if (!c->pol_graph || key != c->pol_graph_key) {
+      if (c->pol_graph) {
+        (void)hipGraphExecDestroy(c->pol_graph);
+        c->pol_graph = nullptr;
+      }
+      hipGraph_t g = nullptr;
+      HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+      const int erc = enqueue();
+      const hipError_t ce = hipStreamEndCapture(c->stream, &g);
+      if (erc != CCKA_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return erc;
+      }
+      HIPCHK(c, ce);
+      const hipError_t ie = hipGraphInstantiate(&c->pol_graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      HIPCHK(c, ie);
+      c->pol_graph_key = key;
     }
-    k.t0 = t;
-    k.t1 = t + 1;
-    k.state_load = 1;
-    HIPCHK(c, launch_rollout(k, block, lds, c->stream));
-    if ((rc = keep_feat(t + 1)) != CCKA_OK) return rc;
+    HIPCHK(c, hipGraphLaunch(c->pol_graph, c->stream));
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   // back to whole-horizon rollouts with the scenarios' own overrides
@@ -1960,6 +2025,14 @@ int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
 }
 
 // Internal: scenarios per wave of the single-deployment kernel (1..64; 0 = automatic).
+// Internal: 0 = enqueue the closed loop's launches directly instead of
+// replaying its captured hipGraph (1, the default)
+int ccka_debug_policy_graph(ccka_ctx* c, int32_t on) {
+  if (!c) return CCKA_EINVAL;
+  c->pol_graph_off = on == 0;
+  return CCKA_OK;
+}
+
 int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
   if (!c || lpw < 0 || lpw > 64) return CCKA_EINVAL;
   c->lpw = lpw;

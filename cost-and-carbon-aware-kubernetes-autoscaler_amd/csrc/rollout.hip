@@ -300,6 +300,15 @@ __device__ __forceinline__ Dep load_dep(const ccka_deployment* d) {
   return o;
 }
 
+// Percent policy factor 1 +/- value/100 exactly as the spec writes it, made
+// where it is used: the asm redefines the value, so the compiler cannot hoist
+// the binary64 factors out of the step loop (four of them held across it
+// spilled to scratch in the occupancy-2 instantiation)
+__device__ __forceinline__ double pct_factor(int value, bool up) {
+  asm volatile("" : "+v"(value));
+  return up ? 1.0 + (double)value / 100.0 : 1.0 - (double)value / 100.0;
+}
+
 // rate limit of one direction (convertDesiredReplicasWithBehaviorRate)
 __device__ __forceinline__ int rate_limit(const Rule& R, bool up, int cur, const int* delta) {
   if (R.sel == CCKA_SELECT_DISABLED) return cur;
@@ -320,8 +329,8 @@ __device__ __forceinline__ int rate_limit(const Rule& R, bool up, int cur, const
     if (R.type[q] == CCKA_HPA_PODS) pr = up ? pst + R.value[q] : pst - R.value[q];
     // Percent: 1 +/- value/100 computed exactly as the spec writes it (on use:
     // rare, and no registers held across the step loop)
-    else if (up) pr = (int)ceil((double)pst * (1.0 + (double)R.value[q] / 100.0));
-    else pr = (int)((double)pst * (1.0 - (double)R.value[q] / 100.0));
+    else if (up) pr = (int)ceil((double)pst * pct_factor(R.value[q], true));
+    else pr = (int)((double)pst * pct_factor(R.value[q], false));
     res = (up == min_sel) ? min(res, pr) : max(res, pr);
   }
   return (int)res;
@@ -393,8 +402,8 @@ __device__ int rate_long(const ccka_hpa_rules* R, bool up, int cur, int sync_s, 
     const long long pst = (long long)cur - add + rem;
     long long pr;
     if (P.type == CCKA_HPA_PODS) pr = up ? pst + P.value : pst - P.value;
-    else if (up) pr = (int)ceil((double)pst * (1.0 + (double)P.value / 100.0));
-    else pr = (int)((double)pst * (1.0 - (double)P.value / 100.0));
+    else if (up) pr = (int)ceil((double)pst * pct_factor(P.value, true));
+    else pr = (int)((double)pst * pct_factor(P.value, false));
     res = (up == min_sel) ? min(res, pr) : max(res, pr);
   }
   return (int)res;

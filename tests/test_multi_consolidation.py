@@ -152,3 +152,30 @@ def test_gpu_two_to_one(engine):
     rc, tc = po.rollout(spec, ScenarioSet(1), load, traj=True)
     compare(rg, rc, tg, tc)
     assert rg["final_nodes"][0] == 1 and rg["last_choice"][0] & 0xFFF == k["c6i.xlarge"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("budget,engine_id", [(10, 2), (12, 2), (13, 1), (25, 1)])
+def test_gpu_multi_under_reference_budgets(engine, budget, engine_id):
+    """The reference's upstream defaults together (15 s HPA sync, drift and
+    replacement at the zone switch, multi-node consolidation for the
+    WhenEmptyOrUnderutilized pool, demo_20_offpeak_configure.sh:59) at the
+    config-2 node count: with a budget of <= 1 node per step for any pool size
+    (ceil(pct * 8 / 100) <= 1, the reference's 10 %) the firstN search has no
+    prefix of >= 2 nodes to try, so the single-deployment kernel runs the
+    world; from 2 nodes on, the general kernel. Bit-exact either way."""
+    spec = configs.config2_world()
+    spec.multi = 1
+    spec.drift = 1
+    spec.replace = 1
+    spec.hpa_sync_s = 15
+    for p in spec.pools:
+        p.budget_pct = budget
+    sc = configs.hpa_scenarios(1500, first_id=555)
+    load = po.gen_load(configs.trace_gen(13), spec.n_steps, 1, sc.n, first_id=sc.first_id)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == engine_id
+    rc, tc = po.rollout(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
+    if engine_id == 2:
+        assert not ((tc["flags"] & 64) != 0).any()

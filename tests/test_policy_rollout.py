@@ -88,3 +88,36 @@ def test_closed_loop_policy_parity(engine, drift):
         ok = (want_t == at[t]) & (want_c == ac[t])
         assert (ok | near).all(), f"step {t}: {np.count_nonzero(~(ok | near))} actions off"
         assert ok.mean() > 0.98
+
+
+@pytest.mark.gpu
+def test_closed_loop_graph_replay_identical(engine):
+    """The closed loop runs as one captured hipGraph (replayed while its inputs
+    are unchanged): a first call (capture), a second (replay) and a direct
+    launch sequence give bit-identical results, trajectories and actions; new
+    scenarios force a fresh capture."""
+    import ctypes as C
+    spec, sc, load = _case(drift=0)
+    ws, bs = configs.mlp_weights(11)
+    engine.set_world(spec)
+    engine.set_scenarios(sc)
+    engine.set_load(load)
+    engine.mlp_set_weights([configs.to_bf16_bits(w) for w in ws], bs)
+    fn = engine.lib.ccka_debug_policy_graph
+    fn.argtypes = [C.c_void_p, C.c_int32]
+    runs = []
+    for graph in (1, 1, 0):
+        fn(engine.ctx, graph)
+        engine.policy_rollout(trajectory=True, record=True)
+        runs.append((engine.results(), engine.trajectory(), engine.policy_actions()))
+    fn(engine.ctx, 1)
+    for r, t, (at, ac) in runs[1:]:
+        compare(r, runs[0][0], t, runs[0][1])
+        assert np.array_equal(at, runs[0][2][0]) and np.array_equal(ac, runs[0][2][1])
+    sc2 = configs.hpa_scenarios(sc.n, first_id=777)
+    engine.set_scenarios(sc2)
+    engine.set_load(load)
+    engine.policy_rollout(trajectory=False, record=True)
+    at2, _ = engine.policy_actions()
+    rc, _ = po.rollout_policy(spec, sc2, load, at2, engine.policy_actions()[1], threads=THREADS)
+    compare(engine.results(), rc)
