@@ -47,8 +47,10 @@ def main():
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2)
     ap.add_argument("--n", type=int, default=None, help="scenarios (states) per GPU, overrides the config")
     ap.add_argument("--T", type=int, default=1440)
-    ap.add_argument("--mode", choices=["trajectory", "summary", "policy"], default=None,
-                    help="config 5: 'policy' = the closed-loop policy rollout (MLP in the loop every step)")
+    ap.add_argument("--mode", choices=["trajectory", "summary", "policy", "grad"], default=None,
+                    help="config 5: 'policy' = the closed-loop policy rollout (MLP in the loop every step); "
+                         "'grad' = the differentiable-control step: a stochastic closed-loop rollout plus the "
+                         "score-function gradient of E[cost + w gCO2 + w SLO] (ccka_policy_grad)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--drift", action="store_true",
@@ -119,10 +121,11 @@ def main():
         args.warmup = 50 if cfg == 5 and args.mode != "policy" else (1 if cfg == 5 else 2)
     T = args.T
     spec = sc = None
-    policy = cfg == 5 and args.mode == "policy"
+    policy = cfg == 5 and args.mode in ("policy", "grad")
+    grad = cfg == 5 and args.mode == "grad"
     if policy:
         # closed loop: every step featurize -> MLP (bf16 MFMA) -> actions -> one rollout step
-        N = args.n or 1_000_000
+        N = args.n or (250_000 if grad else 1_000_000)
         T = args.T if args.T != 1440 else 60
         spec = configs.config2_world(n_steps=T)
         sc = configs.hpa_scenarios(N, first_id=rank * N)
@@ -136,8 +139,13 @@ def main():
         fn.argtypes = [C.c_void_p, C.c_int32]
         eng._chk(fn(eng.ctx, 0 if args.no_graph else 1), "ccka_debug_policy_graph")
 
+        grad_obj = []
+
         def step_fn():
-            eng.policy_rollout(trajectory=False)
+            if grad:  # one policy-gradient step's data: rollout + MLP backward over N x T rows
+                grad_obj.append(eng.policy_grad(seed=len(grad_obj) + 1, w_carbon=0.05, w_slo=0.01)[1])
+            else:
+                eng.policy_rollout(trajectory=False)
     elif cfg == 5:
         N = args.n or 10_000_000
         ws, bs = configs.mlp_weights(11)
@@ -223,23 +231,35 @@ def main():
     if policy:
         value = world * N * T * K / elapsed
         # dominant MFMA work: one MLP batch over the N states per rollout step
-        flops = MLP_FLOPS_PER_STATE * N * T
+        # (+ for the gradient: the forward recomputed and the backward over
+        # the N x T rows: dH2 = W3 g, dH1 = W2 dH2, dW1..3, db)
+        flops = MLP_FLOPS_PER_STATE * N * T * (1 if not grad else 2) + \
+            (2 * (256 * 8 + 256 * 256 + 64 * 256 + 256 * 256 + 256 * 8) * N * T if grad else 0)
+        if grad:  # the loop's events do not cover the backward: the whole step's wall time
+            avg_ms = elapsed / K * 1e3
         achieved = flops / (avg_ms * 1e-3) / 1e12
         out = {
-            "metric": "policy-evaluated cluster-steps/sec (closed-loop MLP control policy)",
+            "metric": "policy-evaluated cluster-steps/sec (closed-loop MLP control policy)" if not grad else
+                      "policy-gradient cluster-steps/sec (stochastic closed loop + score-function MLP backward)",
             "value": value, "unit": "cluster-steps/s", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16 MLP (fp32 accumulate) + int64/f64 rollout",
             "data": "synthetic (on-device Philox traces, Xavier-uniform weights seed 11)",
-            "config": {"workload": f"config5 closed loop: {N} clusters x {T} steps, every step featurize -> "
-                                   "MLP 64->256->256->8 -> HPA target + carbon weight -> rollout step",
+            "config": {"workload": (f"config5 closed loop: {N} clusters x {T} steps, every step featurize -> "
+                                    "MLP 64->256->256->8 -> HPA target + carbon weight -> rollout step") if not grad
+                       else (f"config5 differentiable control: {N} clusters x {T} steps, stochastic policy "
+                             "(8 action bins, softmax sampling), objective cost + 0.05 $/kg gCO2 + 0.01 $/SLO-min, "
+                             f"score-function gradient over {N * T} (step, cluster) rows"),
                        "clusters_per_gpu": N, "steps": T, "parallelism": f"data-parallel x{world}",
                        "launch": "direct" if args.no_graph else "hipGraph (captured loop, replayed)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
-                         "kernel": "whole loop (mlp_kernel + policy_act_kernel + rollout_kernel per step)",
+                         "kernel": "whole loop (mlp_kernel + policy_act_kernel + rollout_kernel per step)" if not grad
+                         else "whole step (closed loop + pg_rows_kernel + pg_wgrad_kernel)",
                          "loop_ms_avg": avg_ms, "flops_per_loop": flops},
         }
+        if grad:
+            out["objective_mean_usd"] = grad_obj[-1]
     elif cfg == 5:
         value = world * N * K / elapsed
         flops = MLP_FLOPS_PER_STATE * N

@@ -118,6 +118,6 @@ def test_closed_loop_graph_replay_identical(engine):
     engine.set_scenarios(sc2)
     engine.set_load(load)
     engine.policy_rollout(trajectory=False, record=True)
-    at2, _ = engine.policy_actions()
-    rc, _ = po.rollout_policy(spec, sc2, load, at2, engine.policy_actions()[1], threads=THREADS)
+    at2, ac2 = engine.policy_actions()
+    rc = po.rollout_policy(spec, sc2, load, at2, ac2, threads=THREADS)[0]
     compare(engine.results(), rc)
