@@ -449,6 +449,8 @@ static int d1_prepare(ccka_ctx* c) {
   c->d1.replace = replace ? 1 : 0;
   // beyond the register ring
   if (c->sc_dstab_max > (c->d1.nsub == 4 ? kD1Sync15MaxWindow : CCKA_HIST * CCKA_STEP_SECONDS)) return CCKA_OK;
+  // default behavior and no window beyond 300 s: the 4-record ring instantiation
+  c->d1.he4 = (c->d1.nsub == 1 && c->d1.bdef && c->d1.dstab0 <= 300 && c->sc_dstab_max <= 300) ? 1 : 0;
   const size_t n = (size_t)c->N;
   std::vector<double> wl;
   std::vector<uint8_t> wci;

@@ -216,6 +216,7 @@ struct D1Params {
   const int2* table2;                // [R][24][NZI][3][JT] cheapest offering by price (the G2 offer rule)
   int32_t lds_tab;                   // set by launch_rollout_d1: price tiles, ci and J staged in LDS
   int32_t nsub;                      // HPA decisions per step: 1, or 4 (15 s sync, default behavior)
+  int32_t he4;                       // every down window <= 300 s (a 4-record ring suffices)
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)

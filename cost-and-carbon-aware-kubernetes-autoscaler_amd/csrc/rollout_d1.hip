@@ -482,10 +482,16 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 // NSUB: HPA decisions per step (1, or 4 = the Kubernetes default 15 s sync
 // period, SEMANTICS 3.C sub-steps; upstream default behavior only). The down-
 // stabilisation records then cover 4 decisions per step: HW packed words.
-template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1>
+// HE: down-window records the ring keeps at one decision per step (8, or 4
+// when no scenario's window exceeds 300 s: half the ring, rebuild and hold
+// loops; launch_rollout_d1 picks it from the scenarios' largest window)
+template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1, int HE = 8>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   static_assert(NSUB == 1 || (NSUB == 4 && BDEF && D1_LEAN_V == 2 && D1_HELD_V), "15 s sync: lean default path");
-  constexpr int HW = NSUB == 1 ? 4 : 10;  // history words (2 records each)
+  static_assert(HE == 8 || (HE == 4 && NSUB == 1 && BDEF), "4-record ring: default behavior, one decision per step");
+  constexpr int HW = NSUB == 1 ? HE / 2 : 10;  // history words (2 records each)
+  // steps whose records the event step may rebuild: the window's entries
+  constexpr int JR = NSUB == 1 ? HE : 5;
   uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_last = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   // LDS: per instance type {idle_nw lo, idle_nw hi, dyn_nw_per_m, alloc_cpu_m}
@@ -526,7 +532,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int mx = p.maxr ? (int)p.maxr[i] : p.maxr0;
   const int dwin = p.down_stab ? (int)p.down_stab[i] : p.dstab0;
   // records inside the down window: entries k < (W - 1) / sync (o_entries)
-  const int nd = NSUB == 1 ? __popc(wmask(dwin)) : (dwin > 15 ? min((dwin - 1) / 15, 2 * HW) : 0);
+  const int nd = min(NSUB == 1 ? __popc(wmask(dwin)) : (dwin > 15 ? (dwin - 1) / 15 : 0), 2 * HW);
   const int dnmask = NSUB == 1 ? wmask(dwin) : 0;
   const int reset_ca = p.reset_ca ? (int)p.reset_ca[i] : p.reset_ca0;
   const int pswitch = p.pswitch ? (int)p.pswitch[i] : p.pswitch0;
@@ -974,21 +980,21 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             const uint32_t rr = ((uint32_t)rv & 0xFFFFu) * 0x10001u;
             if (kq >= wl) {  // the whole window is quiet steps (entries >= wl are never read)
 #pragma unroll
-              for (int w = 0; w < 4; ++w) hdn[w] = rr;
+              for (int w = 0; w < HW; ++w) hdn[w] = rr;
             } else {
 #pragma unroll
               for (int j = 1; j < CCKA_HIST; ++j)
-                if (j <= kq) ring_push(hdn, rv);
+                if (j <= kq) ring_push<HW>(hdn, rv);
             }
           } else if (kq > 0) {
             // entry j of the rebuilt window = the record of step t-1-j (j < kq);
             // the rows' samples are read first (independent LDS reads), held
             // proposals are computed only in waves where some lane has one
             const int cur16 = min(replicas, D1_REC_SAT);
-            int us[CCKA_HIST], rv[CCKA_HIST];
+            int us[JR], rv[JR];
             bool anylow = false;
 #pragma unroll
-            for (int j = 0; j < CCKA_HIST; ++j) {
+            for (int j = 0; j < JR; ++j) {
               us[j] = min(ring[ridx(rnext(tr, rbn - 1 - j))], q_rcap);
               rv[j] = q_met ? cur16 : (int)0x8000;
               anylow |= (j < kq) & q_met & (us[j] < q_pge);
@@ -1002,7 +1008,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               const float rbd = __builtin_amdgcn_rcpf((float)dreq);
               bool anyex = false;
 #pragma unroll
-              for (int j = 0; j < CCKA_HIST; ++j) {
+              for (int j = 0; j < JR; ++j) {
                 bool sl = false;
                 const bool low = (j < kq) & q_met & (us[j] < q_pge);
                 const int util = fdiv_nb(us[j] * 100, dreq, rbd, sl);
@@ -1015,13 +1021,13 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               }
               if (__builtin_expect(anyex, 0)) {
 #pragma unroll
-                for (int j = 0; j < CCKA_HIST; ++j)
+                for (int j = 0; j < JR; ++j)
                   if (us[j] >= 0)
                     rv[j] = min((int)ceil(((double)us[j] / (double)target) * (double)rpods), D1_REC_SAT);
               }
             }
 #pragma unroll
-            for (int j = CCKA_HIST - 1; j >= 0; --j)
+            for (int j = JR - 1; j >= 0; --j)
               if (j < kq) {
                 if constexpr (NSUB == 1) ring_push<HW>(hdn, rv[j]);
                 else ring_push4<HW>(hdn, rv[j]);  // the step's NSUB equal records
@@ -2074,12 +2080,14 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
     if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.stamps) {
-    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, q);
+    if (d && p.he4) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true, false, 1, 4>), dim3(grid), dim3(B), lds, s, q);
+    else if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, true>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, true, 2, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.maxn <= 8 && p.NP <= 2 && p.occ == 3) {
     hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 3, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.maxn <= 8 && p.NP <= 2) {
-    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true>), dim3(grid), dim3(B), lds, s, q);
+    if (d && p.he4) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, false, 1, 4>), dim3(grid), dim3(B), lds, s, q);
+    else if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.maxn <= 8) {
     hipLaunchKernelGGL((rollout_d1_kernel<8, 4, false, 2, false>), dim3(grid), dim3(B), lds, s, q);
