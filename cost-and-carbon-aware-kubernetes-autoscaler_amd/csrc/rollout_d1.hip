@@ -325,7 +325,7 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_K_V 2
 #endif
 #ifndef D1_VMN_V
-#define D1_VMN_V 12
+#define D1_VMN_V 8
 #endif
 #ifndef D1_LEAN_V
 #define D1_LEAN_V 2
