@@ -1001,14 +1001,10 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     p.trace_mod = k.trace_mod;
     p.first_id = k.first_id;
     p.NW = c->NW;
+    p.occ = c->occ > 0 ? c->occ : 2;  // higher targets spill (measured slower: tools/occ.py)
     // scenarios per wave: a wave's cost is the union of its lanes' event paths,
     // so when the batch is smaller than one full round of resident waves (two
     // per SIMD at this kernel's register budget) spread it over all of them
-    {
-      const int64_t waves = (c->N + 63) / 64, round = 2LL * 4 * c->cus;
-      p.occ = c->occ > 0 ? c->occ : 2;  // higher targets spill (measured slower: tools/occ.py)
-      (void)waves; (void)round;
-    }
     if (c->lpw > 0) {
       p.lpw = c->lpw;
     } else {

@@ -404,10 +404,14 @@ __device__ __forceinline__ int d1_mod(int x, int n, float rn) {
 // so an out-of-range offset masks a lane's store without an exec-mask branch,
 // and num_records = 0 turns every store off when no trajectory is kept.
 constexpr int D1_NOSTORE = 0x7FFFFFF0;
+// cache policy of the record stores (build variant: 2 = nt, streaming)
+#ifndef D1_NTS_V
+#define D1_NTS_V 0
+#endif
 __device__ __forceinline__ void d1_store_rec(__amdgpu_buffer_rsrc_t r, int voff, const int4& v) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   const i32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, D1_NTS_V);
 }
 
 __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row) {
