@@ -408,10 +408,11 @@ static bool d1_drift_inert(const ccka_ctx* c) {
 // WhenEmptyOrUnderutilized pool: inert when no pool profile uses that policy
 // or no scenario's nodeSelector admits on-demand; multi-node consolidation
 // needs a WhenEmptyOrUnderutilized pool and a budget of >= 2 nodes.
-static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace) {
+static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace, bool* multi) {
   const ccka_world& w = c->hw;
   *drift = !d1_drift_inert(c);
   *replace = false;
+  *multi = false;
   if (*drift && !(w.max_nodes <= 8 && w.n_pools <= 2)) return false;
   bool weou = false;
   for (int q = 0; q < w.n_pools; ++q) {
@@ -431,9 +432,13 @@ static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace) {
     // (SEMANTICS 3.G3). With every pool's disruption budget at <= 1 node for
     // any node count the world allows (ceil(pct * max_nodes / 100) <= 1: the
     // reference's 10 % at 8 nodes) there is no prefix to try, so it never acts
-    // and this kernel is exact; larger budgets run on the general kernel.
-    for (int q = 0; q < w.n_pools; ++q)
-      if ((w.pools[q].budget_pct * w.max_nodes + 99) / 100 >= 2) return false;
+    // and is not evaluated; larger budgets run it in the DRIFT instantiation.
+    bool two = false;
+    for (int q = 0; q < w.n_pools; ++q) two |= (w.pools[q].budget_pct * w.max_nodes + 99) / 100 >= 2;
+    if (two) {
+      if (!(w.max_nodes <= 8 && w.n_pools <= 2)) return false;
+      *multi = true;
+    }
   }
   return true;
 }
@@ -442,11 +447,12 @@ static bool d1_disrupt_ok(const ccka_ctx* c, bool* drift, bool* replace) {
 static int d1_prepare(ccka_ctx* c) {
   c->d1_ready = true;
   c->d1_ok = false;
-  bool drift = false, replace = false;
-  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_ok(c, &drift, &replace)) return CCKA_OK;
-  c->d1.drift = (drift || replace) ? 1 : 0;  // the DRIFT instantiation carries both
+  bool drift = false, replace = false, multi = false;
+  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_ok(c, &drift, &replace, &multi)) return CCKA_OK;
+  c->d1.drift = (drift || replace || multi) ? 1 : 0;  // the DRIFT instantiation carries all three
   c->d1.drift_on = drift ? 1 : 0;
   c->d1.replace = replace ? 1 : 0;
+  c->d1.multi = multi ? 1 : 0;
   // beyond the register ring
   if (c->sc_dstab_max > (c->d1.nsub == 4 ? kD1Sync15MaxWindow : CCKA_HIST * CCKA_STEP_SECONDS)) return CCKA_OK;
   // default behavior and no window beyond 300 s: the 4-record ring instantiation
@@ -486,7 +492,7 @@ static int d1_prepare(ccka_ctx* c) {
   if (hipMalloc((void**)&c->d_table, keys * c->NW * c->JT * sizeof(int2)) != hipSuccess ||
       hipMalloc((void**)&c->d_jtab, keys * sizeof(int32_t)) != hipSuccess)
     return fail(c, CCKA_ENOMEM, "argmin table alloc (%zu keys x %d weights x %d)", keys, c->NW, c->JT);
-  if (replace) {  // the G2 offer table: cheapest offering holding n pods, by price
+  if (replace || multi) {  // the G2 / G3 offer table: cheapest offering holding n pods, by price
     const double zero = 0.0;
     if ((rc = dupload(c, c->d_wc0, &zero, 1)) != CCKA_OK) return rc;
     if (hipMalloc((void**)&c->d_table2, keys * c->JT * sizeof(int2)) != hipSuccess ||
@@ -1022,7 +1028,7 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, launch_table(tp, c->stream));
     p.table2 = nullptr;
-    if (p.replace) {  // the G2 offer table (price only)
+    if (p.replace || p.multi) {  // the G2 / G3 offer table (price only)
       TableParams t2 = tp;
       t2.wc1000 = c->d_wc0;
       t2.NW = 1;

@@ -217,6 +217,7 @@ struct D1Params {
   int32_t lds_tab;                   // set by launch_rollout_d1: price tiles, ci and J staged in LDS
   int32_t nsub;                      // HPA decisions per step: 1, or 4 (15 s sync, default behavior)
   int32_t he4;                       // every down window <= 300 s (a 4-record ring suffices)
+  int32_t multi;                     // 1: multi-node consolidation (SEMANTICS 3.G3) acts (DRIFT instantiation)
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)

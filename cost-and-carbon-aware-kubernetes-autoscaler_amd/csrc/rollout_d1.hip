@@ -404,6 +404,14 @@ __device__ __forceinline__ int d1_mod(int x, int n, float rn) {
 // so an out-of-range offset masks a lane's store without an exec-mask branch,
 // and num_records = 0 turns every store off when no trajectory is kept.
 constexpr int D1_NOSTORE = 0x7FFFFFF0;
+// wave priority (build variant): 1 = raised during event runs, 2 = raised
+// outside them (quiet steps and the loop)
+#ifndef D1_PRIO_V
+#define D1_PRIO_V 0
+#endif
+#ifndef D1_PRIO_HI
+#define D1_PRIO_HI 2
+#endif
 // cache policy of the record stores (build variant: 2 = nt, streaming)
 #ifndef D1_NTS_V
 #define D1_NTS_V 0
@@ -489,7 +497,10 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 // HE: down-window records the ring keeps at one decision per step (8, or 4
 // when no scenario's window exceeds 300 s: half the ring, rebuild and hold
 // loops; launch_rollout_d1 picks it from the scenarios' largest window)
-template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1, int HE = 8>
+// G3: the DRIFT instantiation with multi-node consolidation (budgets of >= 2
+// nodes; its trial copies of the slots would spill in the others)
+template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1, int HE = 8,
+          bool G3 = false>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   static_assert(NSUB == 1 || (NSUB == 4 && BDEF && D1_LEAN_V == 2 && D1_HELD_V), "15 s sync: lean default path");
   static_assert(HE == 8 || (HE == 4 && NSUB == 1 && BDEF), "4-record ring: default behavior, one decision per step");
@@ -564,7 +575,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const GLOBAL_AS double* const ci_gpwmin = opq_ptr(p.ci_gpwmin);
   const GLOBAL_AS int2* const table = opq_ptr(p.table);
   const GLOBAL_AS int2* const table2 = opq_ptr(p.table2);
-  const int drift_on = opq(p.drift_on), replace = opq(p.replace);
+  const int drift_on = opq(p.drift_on), replace = opq(p.replace), multi = G3 ? opq(p.multi) : 0;
   const GLOBAL_AS int32_t* const jtab = opq_ptr(p.jtab);
   GLOBAL_AS int4* const traj = opq_ptr(reinterpret_cast<int4*>(p.traj));
   // BDEF: the upstream default behavior as compile-time constants
@@ -957,6 +968,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     const uint64_t sb = __ballot(stall);
     if constexpr (STAMPS) st_acc[9] += 1;
     if (sb != 0 && (it % D1_K == D1_K - 1 || !qadv)) {
+      if constexpr (D1_PRIO_V == 1) __builtin_amdgcn_s_setprio(D1_PRIO_HI);
+      if constexpr (D1_PRIO_V == 2) __builtin_amdgcn_s_setprio(0);
       if constexpr (STAMPS) { st_acc[10] += 1; st_acc[11] += __popcll(sb); }
       // the event step in phases, each a block over the stalled lanes (the
       // wave-uniform points between them carry the diagnostic stamps)
@@ -1295,7 +1308,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         weou_e = weou;
         // G2 (replacement consolidation): on-demand WEOU nodes with pods, not being replaced
         const uint32_t g2c = (DRIFT && replace) ? (weou & od_slots() & ~emp & ~srcm) : 0u;
-        const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)) | g2c);
+        // G3 (multi-node consolidation): WEOU nodes with pods, untainted
+        const uint32_t g3c = (DRIFT && G3 && multi) ? (weou & ~emp & ~taint()) : 0u;
+        const uint32_t gate = elig & (emp | (Ffree >= minscap ? weou : (weou & ~cmask)) | g2c | g3c);
         // DRIFT: ready replacements take over (G1); drifted ready nodes not yet
         // being replaced are drift candidates (G0)
         const uint32_t tkm = DRIFT ? (repm & rdy) : 0u;
@@ -1346,8 +1361,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           };
           if constexpr (DRIFT) {
             if (tkm) {
-              // G1: each ready replacement (slot order) takes its source's pods up
-              // to its free capacity; the rest are evicted; the source is deleted
+              // G1: each ready replacement (slot order) takes its sources' pods
+              // (sources in slot order; sinfo bits 16..23 = the source mask) up to
+              // its free capacity; the rest are evicted; the sources are deleted
               uint32_t tk = tkm;
               while (tk) {
                 const int m = __ffs((int)tk) - 1;
@@ -1357,18 +1373,25 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n)
                   if (n == m) { xm = sinfo[n]; sinfo[n] = xm & 0xFFFFu; capm = scap[n]; podm = spods[n]; }
-                const int src = (int)(xm >> 16 & 31u) - 1;
-                int sp = 0;
+                const bool okc = (capbit1((int)(xm >> 12 & 1u)) & capsel) != 0;
+                uint32_t sm = xm >> 16 & 0xFFu;
+                int got = 0;
+                while (sm) {
+                  const int src = __ffs((int)sm) - 1;
+                  sm &= sm - 1;
+                  int sp = 0;
 #pragma unroll
-                for (int n = 0; n < MAXN; ++n) sp = n == src ? spods[n] : sp;
-                const int k = (capbit1((int)(xm >> 12 & 1u)) & capsel) ? min(capm - podm, sp) : 0;
+                  for (int n = 0; n < MAXN; ++n) sp = n == src ? spods[n] : sp;
+                  const int k = okc ? min(capm - podm - got, sp) : 0;
+                  got += k;
+                  rpods -= sp - k;
+                  placed -= sp - k;
+                  drop_slot(src);
+                }
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n)
-                  if (n == m) { spods[n] += k; slc[n] = t + scas[n]; }
-                rpods -= sp - k;
-                placed -= sp - k;
+                  if (n == m) { spods[n] += got; slc[n] = t + scas[n]; }
                 repm &= ~(1u << m);
-                drop_slot(src);
                 flags |= 4u;
               }
               ffree_now();
@@ -1436,7 +1459,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
                   for (int n = 0; n < MAXN; ++n) {
                     if (n == slot) {
-                      sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13 | (best + 1) << 16);
+                      sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13) | (1u << (16 + best));
                       sready[n] = rs;
                       slc[n] = t + casc(cq);
                       scas[n] = casc(cq);
@@ -1569,11 +1592,165 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 emp = em & used;
               }
             }
+            // G3 (SEMANTICS 3.G3): Karpenter's firstN binary search over the
+            // consolidation order (pods asc, price desc, slot asc) for the longest
+            // prefix of >= 2 candidates that leaves together: their pods move
+            // first-fit onto the other compatible ready untainted slots, the rest
+            // needs one new node strictly cheaper than the set (the offer table,
+            // no spot when every candidate is spot) in a free slot
+            bool g3_acted = false;
+            if constexpr (DRIFT && G3) {
+              if (multi && weou_q && deleted < qbudget) {
+                const uint32_t tn = taint();
+                const uint32_t cset = elig & pmask[q] & ~emp & ~tn;
+                const int nc = min(__popc(cset), qbudget - deleted);
+                if (nc >= 2) {
+                  uint32_t ord = 0;  // nibble r = slot of rank r
+#pragma unroll
+                  for (int n = 0; n < MAXN; ++n) {
+                    int rk = 0;
+#pragma unroll
+                    for (int m = 0; m < MAXN; ++m) {
+                      const bool before = spods[m] < spods[n] ||
+                                          (spods[m] == spods[n] && (sprice[m] > sprice[n] || (sprice[m] == sprice[n] && m < n)));
+                      rk += ((cset >> m & 1u) && before) ? 1 : 0;
+                    }
+                    ord |= (cset >> n & 1u) ? (uint32_t)n << (4 * rk) : 0u;
+                  }
+                  uint32_t cmq = 0;
+                  int zq = -1, cq = 0;
+#pragma unroll
+                  for (int qq = 0; qq < MAXP; ++qq)
+                    if (qq == q) { zq = pzi[qq]; cmq = pcm[qq] & capsel; cq = pcas[qq]; }
+                  const uint32_t fr = ~used & slot_mask;
+                  int lo = 1, hi = nc - 1, bestk = 0, mid = 0;
+                  while (true) {
+                    int k;
+                    bool commit = false;
+                    if (lo <= hi) { mid = (lo + hi) / 2; k = mid + 1; }
+                    else if (bestk) { k = bestk; commit = true; }
+                    else break;
+                    uint32_t set = 0;
+                    for (int r = 0; r < k; ++r) set |= 1u << (ord >> (4 * r) & 15u);
+                    int tp[MAXN];
+                    int pdbp = 0, psum = 0;
+                    uint32_t anyod = 0;
+#pragma unroll
+                    for (int n = 0; n < MAXN; ++n) {
+                      tp[n] = spods[n];
+                      const bool in = set >> n & 1u;
+                      pdbp += in ? spods[n] : 0;
+                      psum += in ? sprice[n] : 0;
+                      anyod |= in ? (sinfo[n] >> 12 & 1u) : 0u;
+                    }
+                    bool ok = !(pdb_member && pdbp > allowed);
+                    uint32_t touched = 0;
+                    const uint32_t recv = rdy & ~tn & ~set & cmask;
+                    for (int r = 0; r < k; ++r) {
+                      const int c = (int)(ord >> (4 * r) & 15u);
+                      int need = 0;
+#pragma unroll
+                      for (int n = 0; n < MAXN; ++n) need = n == c ? tp[n] : need;
+#pragma unroll
+                      for (int m = 0; m < MAXN; ++m) {
+                        const int f = (recv >> m & 1u) ? scap[m] - tp[m] : 0;
+                        const int kk = min(f, need);
+                        tp[m] += kk;
+                        need -= kk;
+                        touched |= (kk > 0 ? 1u : 0u) << m;
+                      }
+#pragma unroll
+                      for (int n = 0; n < MAXN; ++n) tp[n] = n == c ? need : tp[n];
+                    }
+                    int sp = 0;
+#pragma unroll
+                    for (int n = 0; n < MAXN; ++n) sp += (set >> n & 1u) ? tp[n] : 0;
+                    int2 e = make_int2(0, -1);
+                    if (ok && sp > 0) {
+                      const uint32_t cm = anyod ? cmq : (cmq & ~(uint32_t)CCKA_CAP_SPOT);
+                      ok = cm != 0 && fr != 0 && zq >= 0 && sp < JT;
+                      if (ok) e = d1_tload(table2 + (((int64_t)rh * NZI + zq) * 3 + (cm - 1)) * JT + sp);
+                      ok = ok && e.y >= 0 && e.x < psum;
+                    }
+                    if (!commit) {
+                      if (ok) { bestk = k; lo = mid + 1; }
+                      else hi = mid - 1;
+                      continue;
+                    }
+                    // commit: the moves, emptied candidates leave now, the others
+                    // when the replacement is ready (G1)
+                    uint32_t srcmask = 0;
+#pragma unroll
+                    for (int n = 0; n < MAXN; ++n) {
+                      spods[n] = tp[n];
+                      slc[n] = (touched >> n & 1u) ? t + scas[n] : slc[n];
+                      srcmask |= ((set >> n & 1u) && tp[n] > 0 ? 1u : 0u) << n;
+                    }
+                    uint32_t gone = set & ~srcmask;
+                    while (gone) {
+                      const int n = __ffs((int)gone) - 1;
+                      gone &= gone - 1;
+                      drop_slot(n);
+                      flags |= 4u;
+                    }
+                    if (sp > 0) {
+                      const int info = e.y, prc = e.x;
+                      const int bk = info & 1023, bz = info >> 10 & 3, bc = info >> 12 & 1, cap1 = info >> 16;
+                      const int slot = __ffs((int)fr) - 1;
+                      const int rs = t + delay;
+                      const int4 ac = s_acc[bk];
+#pragma unroll
+                      for (int n = 0; n < MAXN; ++n) {
+                        if (n == slot) {
+                          sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13) | (srcmask << 16);
+                          sready[n] = rs;
+                          slc[n] = t + casc(cq);
+                          scas[n] = casc(cq);
+                          spods[n] = 0;
+                          sprice[n] = prc;
+                          scap[n] = cap1;
+                          sdyn[n] = (uint32_t)ac.z;
+                          salloc[n] = ac.w;
+                          sallocr[n] = delay == 0 ? ac.w : 0;
+                        }
+                      }
+                      const uint32_t bit = 1u << slot;
+                      used |= bit;
+                      if (capbit1(bc) & capsel) cmask |= bit;
+#pragma unroll
+                      for (int qq = 0; qq < MAXP; ++qq) if (qq == q) pmask[qq] |= bit;
+                      if (delay == 0) rdy |= bit;
+                      else next_ready = min(next_ready, rs);
+                      minscap = min(minscap, cap1);
+                      Isum += ((long long)ac.y << 32) | (unsigned)ac.x;
+                      if (bc == 0) nsp++; else nod++;
+                      burn += prc;
+                      launches++;
+                      last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+                      hash = (hash ^ last_choice) * 16777619u;
+                      step_last_type = bk;
+                      srcm |= srcmask;
+                      repm |= bit;
+                      flags |= 2u | 32u;
+                    }
+                    flags |= 64u;
+                    if (pdb_member) allowed -= pdbp;
+                    deleted += k;
+                    any_del = true;
+                    g_acted = true;
+                    g3_acted = true;
+                    ffree_now();
+                    masks_now();
+                    break;
+                  }
+                }
+              }
+            }
             if constexpr (DRIFT) {
               // G2: the first candidate (pods asc, price desc, slot asc) with a
               // strictly cheaper single offering for its pods gets a pre-spun
               // replacement (the offer table: price only); one per pool per step
-              if (replace && weou_q && deleted < qbudget) {
+              if (replace && weou_q && !g3_acted && deleted < qbudget) {
                 uint32_t c2 = elig & pmask[q] & od_slots() & ~emp & ~srcm;
                 while (c2) {
                   unsigned long long bkey = ~0ull;
@@ -1607,7 +1784,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
                   for (int n = 0; n < MAXN; ++n) {
                     if (n == slot) {
-                      sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13 | (best + 1) << 16);
+                      sinfo[n] = (uint32_t)(bk | bz << 10 | bc << 12 | q << 13) | (1u << (16 + best));
                       sready[n] = rs;
                       slc[n] = t + casc(cq);
                       scas[n] = casc(cq);
@@ -1814,7 +1991,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           // empty slots and WhenEmptyOrUnderutilized pools as the disruption
           // phase left them (deletions only clear bits that rdy clears too)
           const uint32_t gm = rdy & (emp_e | (Ffree >= minscap ? weou_e : (weou_e & ~cmask)) |
-                                     ((DRIFT && replace) ? (weou_e & od_slots() & ~emp_e & ~srcm) : 0u));
+                                     ((DRIFT && replace) ? (weou_e & od_slots() & ~emp_e & ~srcm) : 0u) |
+                                     ((DRIFT && G3 && multi) ? (weou_e & ~emp_e & ~taint()) : 0u));
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) nx = ((gm >> n & 1u) && slc[n] > t) ? min(nx, slc[n]) : nx;
           if (g_acted || (ablate & 15)) nx = t + 1;  // ablation runs: every step an event
@@ -1828,6 +2006,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       pf_ok = pf_ok && !ev;
       D1_STAMP(7);
     }
+    if constexpr (D1_PRIO_V == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (D1_PRIO_V == 2) __builtin_amdgcn_s_setprio(D1_PRIO_HI);
     // ---- ring refill: D1_S rows per iteration once every lane has consumed
     // what they overwrite; issued after the event steps, whose own loads
     // wait for every older vector-memory operation ----
@@ -2078,8 +2258,12 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
   if (p.nsub == 4) {  // 15 s HPA sync, default behavior (d1_check_world)
-    if (p.drift) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 4>), dim3(grid), dim3(B), lds, s, q);
+    if (p.multi) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 4, 8, true>), dim3(grid), dim3(B), lds, s, q);
+    else if (p.drift) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 4>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, false, 4>), dim3(grid), dim3(B), lds, s, q);
+  } else if (p.multi) {  // + multi-node consolidation (SEMANTICS 3.G3)
+    if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 1, 8, true>), dim3(grid), dim3(B), lds, s, q);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true, 1, 8, true>), dim3(grid), dim3(B), lds, s, q);
   } else if (p.drift) {  // drift (SEMANTICS 3.G0): 8 slots, <= 2 pools (d1_disrupt_ok)
     if (d) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, false, true>), dim3(grid), dim3(B), lds, s, q);

@@ -9,7 +9,7 @@ import pytest
 
 import pyoracle as po
 from ccka import abi, configs
-from ccka.world import ScenarioSet, deployment
+from ccka.world import ScenarioSet, deployment, hpa_rules
 from parity import compare, run_engine
 from test_oracle_kat import tiny_world
 
@@ -155,15 +155,15 @@ def test_gpu_two_to_one(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("budget,engine_id", [(10, 2), (12, 2), (13, 1), (25, 1)])
-def test_gpu_multi_under_reference_budgets(engine, budget, engine_id):
+@pytest.mark.parametrize("budget", [10, 12, 13, 25])
+def test_gpu_multi_under_reference_budgets(engine, budget):
     """The reference's upstream defaults together (15 s HPA sync, drift and
     replacement at the zone switch, multi-node consolidation for the
     WhenEmptyOrUnderutilized pool, demo_20_offpeak_configure.sh:59) at the
-    config-2 node count: with a budget of <= 1 node per step for any pool size
-    (ceil(pct * 8 / 100) <= 1, the reference's 10 %) the firstN search has no
-    prefix of >= 2 nodes to try, so the single-deployment kernel runs the
-    world; from 2 nodes on, the general kernel. Bit-exact either way."""
+    config-2 node count, on the single-deployment kernel: with a budget of <= 1
+    node per step for any pool size (ceil(pct * 8 / 100) <= 1, the reference's
+    10 %) the firstN search has no prefix of >= 2 nodes to try (no G3 at all),
+    from 2 nodes on its G3 instantiation runs it. Bit-exact either way."""
     spec = configs.config2_world()
     spec.multi = 1
     spec.drift = 1
@@ -174,8 +174,64 @@ def test_gpu_multi_under_reference_budgets(engine, budget, engine_id):
     sc = configs.hpa_scenarios(1500, first_id=555)
     load = po.gen_load(configs.trace_gen(13), spec.n_steps, 1, sc.n, first_id=sc.first_id)
     rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
-    assert engine.last_engine()[0] == engine_id
+    assert engine.last_engine()[0] == 2
     rc, tc = po.rollout(spec, sc, load, traj=True, threads=THREADS)
     compare(rg, rc, tg, tc)
-    if engine_id == 2:
+    if budget <= 12:
         assert not ((tc["flags"] & 64) != 0).any()
+
+
+def _d1_multi_world(name):
+    """8 slots, both pools WhenEmptyOrUnderutilized, budgets admitting >= 2
+    nodes: multi-node consolidation in the single-deployment kernel."""
+    spec = configs.config2_world()
+    spec.multi = 1
+    for p in spec.pools:
+        p.budget_pct = 100
+    for pr in (abi.PROFILE_RESET, abi.PROFILE_OFFPEAK, abi.PROFILE_PEAK):
+        spec.pools[0].profile[pr].policy = abi.WHEN_EMPTY_OR_UNDERUTILIZED
+        spec.pools[1].profile[pr].policy = abi.WHEN_EMPTY_OR_UNDERUTILIZED
+    sc = configs.hpa_scenarios(1200, first_id=77)
+    if name == "pdb":
+        spec.pdb_pct = 50
+    elif name == "budget50":
+        for p in spec.pools:
+            p.budget_pct = 50
+    elif name == "delay0":
+        spec.provision_delay_steps = 0
+        spec.pdb_pct = -1
+    elif name == "drift_replace":
+        spec.drift = 1
+        spec.replace = 1
+        spec.pdb_pct = -1
+    elif name == "sync15":
+        spec.hpa_sync_s = 15
+        spec.pdb_pct = -1
+    elif name == "no_pdb":
+        spec.pdb_pct = -1
+    elif name == "custom_rules":
+        spec.pdb_pct = -1
+        spec.deploys = [deployment(abi.SCALER_HPA, down=hpa_rules(abi.SELECT_MAX, [(abi.HPA_PODS, 2, 60)], 120))]
+    return spec, sc
+
+
+D1_VARIANTS = ["pdb", "budget50", "delay0", "drift_replace", "sync15", "no_pdb", "custom_rules"]
+
+
+@pytest.mark.parametrize("variant", D1_VARIANTS)
+def test_oracle_d1_multi_worlds_act(variant):
+    spec, sc = _d1_multi_world(variant)
+    load = po.gen_load(configs.trace_gen(17), spec.n_steps, 1, sc.n, first_id=sc.first_id)
+    _, tc = po.rollout(spec, sc, load, traj=True, threads=8)
+    assert ((tc["flags"] & 64) != 0).any(), "no multi-node consolidation happened"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", D1_VARIANTS)
+def test_gpu_multi_single_deployment_kernel(engine, variant):
+    spec, sc = _d1_multi_world(variant)
+    load = po.gen_load(configs.trace_gen(17), spec.n_steps, 1, sc.n, first_id=sc.first_id)
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    rc, tc = po.rollout(spec, sc, load, traj=True, threads=THREADS)
+    compare(rg, rc, tg, tc)
