@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--multi", action="store_true",
                     help="configs 2-4 with multi-node consolidation (SEMANTICS 3.G3, Karpenter's default for "
                          "WhenEmptyOrUnderutilized pools)")
+    ap.add_argument("--budget", type=int, default=None,
+                    help="NodePool disruption budget in %% of the pool's nodes (default: the reference's 10)")
     ap.add_argument("--hpa-sync", type=int, default=0, choices=[0, 10, 15, 20, 30, 60],
                     help="HPA decision period in seconds (Kubernetes default 15: four decisions per one-minute "
                          "step; 0 = one per step)")
@@ -179,6 +181,9 @@ def main():
         spec.replace = int(args.replace)
         spec.multi = int(args.multi)
         spec.hpa_sync_s = args.hpa_sync
+        if args.budget is not None:
+            for pool in spec.pools:
+                pool.budget_pct = args.budget
         eng.set_world(spec)
         eng.set_scenarios(sc)
         eng.gen_load(gen)
@@ -312,13 +317,15 @@ def main():
             "config": {"workload": workloads[cfg] + (" + Karpenter drift at the zone switch" if args.drift else "")
                        + (" + replacement consolidation" if args.replace else "")
                        + (" + multi-node consolidation" if args.multi else "")
-                       + (f" + HPA sync every {args.hpa_sync} s" if args.hpa_sync not in (0, 60) else ""),
+                       + (f" + HPA sync every {args.hpa_sync} s" if args.hpa_sync not in (0, 60) else "")
+                       + (f", disruption budget {args.budget} %" if args.budget is not None else ""),
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
                        "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None if args.drift or args.replace or args.multi or args.hpa_sync not in (0, 60)
+                         or args.budget is not None
                          else measured_traffic(cfg, traj, N, T),
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,

@@ -404,13 +404,15 @@ __device__ __forceinline__ int d1_mod(int x, int n, float rn) {
 // so an out-of-range offset masks a lane's store without an exec-mask branch,
 // and num_records = 0 turns every store off when no trajectory is kept.
 constexpr int D1_NOSTORE = 0x7FFFFFF0;
-// wave priority (build variant): 1 = raised during event runs, 2 = raised
-// outside them (quiet steps and the loop)
+// wave priority: 1 = raised during event runs, 2 = raised outside them (quiet
+// steps and the loop). Every variant measured 4 % faster than none, whatever
+// the level and direction (tools/variant_bench.py: 1.815-1.827 vs 1.904 ms),
+// so the gain is as much the s_setprio boundaries as the arbitration
 #ifndef D1_PRIO_V
-#define D1_PRIO_V 0
+#define D1_PRIO_V 2
 #endif
 #ifndef D1_PRIO_HI
-#define D1_PRIO_HI 2
+#define D1_PRIO_HI 3
 #endif
 // cache policy of the record stores (build variant: 2 = nt, streaming)
 #ifndef D1_NTS_V
