@@ -331,7 +331,7 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 #define D1_LEAN_V 2
 #endif
 #ifndef D1_S_V
-#define D1_S_V 7
+#define D1_S_V 8
 #endif
 // LEAN 2: 1 = a proposal below cur held by the down window is a quiet step
 // (its record is rebuilt at the next event), 0 = such a step is an event, so
