@@ -1635,7 +1635,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                     uint32_t set = 0;
                     for (int r = 0; r < k; ++r) set |= 1u << (ord >> (4 * r) & 15u);
                     int tp[MAXN];
-                    int pdbp = 0, psum = 0;
+                    int pdbp = 0;
+                    long long psum = 0;  // up to 8 hourly prices (int64 as in the oracle)
                     uint32_t anyod = 0;
 #pragma unroll
                     for (int n = 0; n < MAXN; ++n) {
@@ -1672,7 +1673,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                       const uint32_t cm = anyod ? cmq : (cmq & ~(uint32_t)CCKA_CAP_SPOT);
                       ok = cm != 0 && fr != 0 && zq >= 0 && sp < JT;
                       if (ok) e = d1_tload(table2 + (((int64_t)rh * NZI + zq) * 3 + (cm - 1)) * JT + sp);
-                      ok = ok && e.y >= 0 && e.x < psum;
+                      ok = ok && e.y >= 0 && (long long)e.x < psum;
                     }
                     if (!commit) {
                       if (ok) { bestk = k; lo = mid + 1; }
