@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 STEP_SECONDS = 60
 MAX_TYPES = 1024
 MAX_ZONES = 4
@@ -118,7 +118,7 @@ class Totals(C.Structure):
     _fields_ = [("scenarios", C.c_int64), ("cost_uphmin", C.c_int64), ("slo_minutes", C.c_int64),
                 ("pending_pod_minutes", C.c_int64), ("node_min_spot", C.c_int64),
                 ("node_min_od", C.c_int64), ("launches", C.c_int64), ("deletions", C.c_int64),
-                ("energy_nwmin", C.c_int64), ("gco2_ug", C.c_int64),
+                ("energy_uwmin", C.c_int64), ("gco2_ug", C.c_int64),
                 ("energy_wmin", C.c_double), ("gco2", C.c_double)]
 
 
@@ -243,6 +243,8 @@ def load_engine(path: str | None = None):
         "ccka_comm_init": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int32, C.c_int32]),
         "ccka_allreduce_totals": (C.c_int, [vp, C.POINTER(Totals)]),
         "ccka_comm_info": (C.c_int, [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+        "ccka_totals_pack": (C.c_int, [C.POINTER(Totals), C.c_int32, C.POINTER(C.c_int64), C.c_int32]),
+        "ccka_totals_finish": (C.c_int, [C.POINTER(C.c_int64), C.c_int32, C.POINTER(Totals)]),
         "ccka_device_info": (C.c_int, [vp, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
@@ -263,8 +265,10 @@ EXPORTED = [
     "ccka_mlp_set_weights", "ccka_mlp_set_states", "ccka_mlp_gen_states", "ccka_mlp_forward",
     "ccka_mlp_forward_async", "ccka_mlp_get_actions", "ccka_set_detail", "ccka_get_detail",
     "ccka_policy_rollout", "ccka_get_policy_actions", "ccka_trajectory_layout", "ccka_get_trajectory_native",
-    "ccka_policy_grad", "ccka_get_policy_samples", "ccka_mlp_backward",
+    "ccka_policy_grad", "ccka_get_policy_samples", "ccka_mlp_backward", "ccka_totals_pack", "ccka_totals_finish",
 ]
+TOTALS_INT64, TOTALS_BLOCK = 10, 11  # CCKA_TOTALS_INT64, CCKA_TOTALS_BLOCK
+EOVERFLOW = -8
 TRAJ_TN, TRAJ_NT = 0, 1  # device layouts of the trajectory records (ccka_trajectory_layout)
 
 

@@ -147,6 +147,8 @@ struct ccka_ctx {
   uint8_t* d_pg_act = nullptr;   // sampled actions [T][N] (or the rows of ccka_mlp_backward)
   int64_t pg_act_count = 0;
   float* d_pg_coef = nullptr;    // per-scenario (J - b) / N (or per row)
+  uint64_t* d_pg_seed = nullptr; // the sampling key of the stochastic loop (outside the graph key)
+  uint64_t pg_seed_host = 0;
   int64_t pg_coef_count = 0;
   uint16_t* d_pg_x = nullptr;    // ccka_mlp_backward's rows [M][64]
   int64_t pg_x_count = 0;
@@ -583,7 +585,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_pol_state); dfree(c->d_pol_target); dfree(c->d_pol_cw); dfree(c->d_rec_target); dfree(c->d_rec_cw);
   dfree(c->d_feat_rec);
   dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
-  dfree(c->d_w2b); dfree(c->d_w3b); dfree(c->d_pg_act); dfree(c->d_pg_coef); dfree(c->d_pg_x);
+  dfree(c->d_w2b); dfree(c->d_w3b); dfree(c->d_pg_act); dfree(c->d_pg_coef); dfree(c->d_pg_seed); dfree(c->d_pg_x);
   dfree(c->d_pg_work); dfree(c->d_pg_part); dfree(c->d_pg_grad);
   free_results(c);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -703,7 +705,7 @@ static int alloc_results(ccka_ctx* c) {
   k.final_nodes = (int32_t*)p; p += b4;
   k.last_choice = (uint32_t*)p; p += b4;
   k.hash = (uint32_t*)p; p += b4;
-  if (hipMalloc(&c->d_parts, 1024 * sizeof(long long) * 10) != hipSuccess) return fail(c, CCKA_ENOMEM, "parts alloc");
+  if (hipMalloc(&c->d_parts, (1024 * 11 + 1) * sizeof(long long)) != hipSuccess) return fail(c, CCKA_ENOMEM, "parts alloc");
   if (!c->d_totals && hipMalloc((void**)&c->d_totals, sizeof(ccka_totals)) != hipSuccess)
     return fail(c, CCKA_ENOMEM, "totals alloc");
   return CCKA_OK;
@@ -945,6 +947,7 @@ static int setup_general(ccka_ctx* c, int32_t trajectory, int* block_out, size_t
       const int64_t cnt = (int64_t)k.hlen * w.n_deploy * c->N;
       if (c->hist_count < cnt) {
         dfree(c->d_hist);
+        c->hist_count = 0;
         if (hipMalloc((void**)&c->d_hist, (size_t)cnt * sizeof(int2)) != hipSuccess)
           return fail(c, CCKA_ENOMEM, "HPA history alloc (%lld entries)", (long long)cnt);
         c->hist_count = cnt;
@@ -1122,6 +1125,7 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   const int64_t words = state_words(dmax, nmax);
   if (c->pol_state_count < words * N) {
     dfree(c->d_pol_state);
+    c->pol_state_count = 0;
     if (hipMalloc((void**)&c->d_pol_state, (size_t)(words * N) * 4) != hipSuccess)
       return fail(c, CCKA_ENOMEM, "policy state alloc (%lld words)", (long long)(words * N));
     c->pol_state_count = words * N;
@@ -1129,6 +1133,7 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   if (c->pol_n < N) {
     dfree(c->d_pol_target);
     dfree(c->d_pol_cw);
+    c->pol_n = 0;
     if (hipMalloc((void**)&c->d_pol_target, (size_t)N * 2) != hipSuccess ||
         hipMalloc((void**)&c->d_pol_cw, (size_t)N * 8) != hipSuccess)
       return fail(c, CCKA_ENOMEM, "policy action alloc");
@@ -1139,6 +1144,7 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
     if (c->pol_rec_count < (int64_t)T * N) {
       dfree(c->d_rec_target);
       dfree(c->d_rec_cw);
+      c->pol_rec_count = 0;
       if (hipMalloc((void**)&c->d_rec_target, (size_t)T * N * 2) != hipSuccess ||
           hipMalloc((void**)&c->d_rec_cw, (size_t)T * N * 8) != hipSuccess)
         return fail(c, CCKA_ENOMEM, "policy action record alloc");
@@ -1149,6 +1155,7 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   if (pg) {
     if (c->pg_act_count < (int64_t)T * N) {
       dfree(c->d_pg_act);
+      c->pg_act_count = 0;
       if (hipMalloc((void**)&c->d_pg_act, (size_t)T * N) != hipSuccess)
         return fail(c, CCKA_ENOMEM, "policy-gradient action record alloc");
       c->pg_act_count = (int64_t)T * N;
@@ -1157,6 +1164,7 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   if (feat_on) {
     if (c->pol_feat_count < (int64_t)(T + 1) * N * 64) {
       dfree(c->d_feat_rec);
+      c->pol_feat_count = 0;
       if (hipMalloc((void**)&c->d_feat_rec, (size_t)(T + 1) * N * 64 * 2) != hipSuccess)
         return fail(c, CCKA_ENOMEM, "policy feature record alloc");
       c->pol_feat_count = (int64_t)(T + 1) * N * 64;
@@ -1192,7 +1200,12 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
     q0.cw = c->d_pol_cw;
     q0.n = N;
     q0.first_id = c->first_id;
-    q0.seed = pg->seed;
+    if (!c->d_pg_seed && hipMalloc((void**)&c->d_pg_seed, sizeof(uint64_t)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "seed alloc");
+    q0.seed = c->d_pg_seed;
+    // the seed is data, not part of the captured sequence: a new seed replays the graph
+    c->pg_seed_host = pg->seed;
+    HIPCHK(c, hipMemcpyAsync(c->d_pg_seed, &c->pg_seed_host, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   }
   // the whole loop: state initialisation (t = 0, features of step 0), then
   // per step MLP -> actions -> one rollout step (+ the features kept)
@@ -1593,12 +1606,41 @@ int ccka_get_totals(ccka_ctx* c, ccka_totals* out) {
   q.cost = k.cost; q.energy = k.energy; q.gco2 = k.gco2; q.slo = k.slo; q.pend_min = k.pend_min;
   q.nmin_spot = k.nmin_spot; q.nmin_od = k.nmin_od; q.launches = k.launches; q.deletions = k.deletions;
   q.parts = (Part*)c->d_parts;
+  q.ovf = (long long*)c->d_parts + 1024 * 11;
   q.out = c->d_totals;
   q.N = c->N;
   const int nparts = (int)std::min<int64_t>(1024, (c->N + 255) / 256);
+  long long ovf = 0;
   HIPCHK(c, launch_totals(q, nparts, c->stream));
   HIPCHK(c, hipMemcpyAsync(out, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&ovf, q.ovf, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ovf) return fail(c, CCKA_EOVERFLOW, "a fixed-point total exceeds int64 (ccka.h: ccka_totals)");
+  return CCKA_OK;
+}
+
+// ---- the totals exchange, host halves (ccka.h: ccka_totals_pack / _finish) ----
+int ccka_totals_pack(const ccka_totals* in, int32_t nranks, int64_t* block, int32_t n) {
+  if (!in || !block || n != CCKA_TOTALS_BLOCK || nranks < 1) return CCKA_EINVAL;
+  const int64_t* f = &in->scenarios;  // the leading CCKA_TOTALS_INT64 int64 fields
+  static_assert(offsetof(ccka_totals, gco2_ug) == (CCKA_TOTALS_INT64 - 1) * sizeof(int64_t), "int64 block");
+  const int64_t lim = INT64_MAX / nranks;
+  int64_t risk = 0;
+  for (int k = 0; k < CCKA_TOTALS_INT64; ++k) {
+    block[k] = f[k];
+    risk |= (f[k] > lim || f[k] < -lim) ? 1 : 0;
+  }
+  block[CCKA_TOTALS_INT64] = risk;
+  return CCKA_OK;
+}
+
+int ccka_totals_finish(const int64_t* block, int32_t n, ccka_totals* out) {
+  if (!block || !out || n != CCKA_TOTALS_BLOCK) return CCKA_EINVAL;
+  if (block[CCKA_TOTALS_INT64] != 0) return CCKA_EOVERFLOW;
+  int64_t* f = &out->scenarios;
+  for (int k = 0; k < CCKA_TOTALS_INT64; ++k) f[k] = block[k];
+  out->energy_wmin = (double)out->energy_uwmin * 1e-6;
+  out->gco2 = (double)out->gco2_ug * 1e-6;
   return CCKA_OK;
 }
 
@@ -1626,18 +1668,24 @@ int ccka_allreduce_totals(ccka_ctx* c, ccka_totals* io) {
   if (!c || !io) return CCKA_EINVAL;
   if (!c->comm) return fail(c, CCKA_ESTATE, "ccka_comm_init first");
   (void)hipSetDevice(c->device);
+  int nranks = 1;
+  if (ncclCommCount(c->comm, &nranks) != ncclSuccess) return fail(c, CCKA_ERCCL, "ncclCommCount failed");
+  int64_t block[CCKA_TOTALS_BLOCK];
+  if (ccka_totals_pack(io, nranks, block, CCKA_TOTALS_BLOCK) != CCKA_OK) return fail(c, CCKA_EINVAL, "totals pack");
+  // the block goes through the device totals buffer (96 B >= 88 B)
+  static_assert(sizeof(ccka_totals) >= CCKA_TOTALS_BLOCK * sizeof(int64_t), "totals block fits");
   if (!c->d_totals && hipMalloc((void**)&c->d_totals, sizeof(ccka_totals)) != hipSuccess)
     return fail(c, CCKA_ENOMEM, "totals alloc");
-  HIPCHK(c, hipMemcpyAsync(c->d_totals, io, sizeof(ccka_totals), hipMemcpyHostToDevice, c->stream));
-  // the int64 block in one in-place all-reduce (exact, order-independent);
-  // the doubles are re-derived from it, so every rank count gives the same bits
-  const ncclResult_t r = ncclAllReduce(c->d_totals, c->d_totals, CCKA_TOTALS_INT64, ncclInt64, ncclSum,
-                                       c->comm, c->stream);
+  int64_t* d_block = (int64_t*)c->d_totals;
+  HIPCHK(c, hipMemcpyAsync(d_block, block, sizeof block, hipMemcpyHostToDevice, c->stream));
+  // one in-place all-reduce (exact, order-independent); the doubles are
+  // re-derived from the sums, so every rank count gives the same bits
+  const ncclResult_t r = ncclAllReduce(d_block, d_block, CCKA_TOTALS_BLOCK, ncclInt64, ncclSum, c->comm, c->stream);
   if (r != ncclSuccess) return fail(c, CCKA_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-  HIPCHK(c, hipMemcpyAsync(io, c->d_totals, sizeof(ccka_totals), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(block, d_block, sizeof block, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  io->energy_wmin = (double)io->energy_nwmin * 1e-9;
-  io->gco2 = (double)io->gco2_ug * 1e-6;
+  const int st = ccka_totals_finish(block, CCKA_TOTALS_BLOCK, io);
+  if (st != CCKA_OK) return fail(c, st, "a summed total exceeds int64 at %d ranks (ccka.h: ccka_totals)", nranks);
   return CCKA_OK;
 }
 
@@ -1844,6 +1892,8 @@ static int mlp_alloc(ccka_ctx* c, int64_t n) {
   if (c->mlp_cap < n) {
     dfree(c->d_mx);
     dfree(c->d_my);
+    c->mlp_cap = 0;
+    c->mlp_n = 0;
     if (hipMalloc((void**)&c->d_mx, (size_t)n * MLP_IN * 2) != hipSuccess ||
         hipMalloc((void**)&c->d_my, (size_t)n * MLP_OUT * 4) != hipSuccess)
       return fail(c, CCKA_ENOMEM, "MLP state/action buffers (%lld states)", (long long)n);

@@ -98,10 +98,11 @@ struct TotParams {
   const int32_t* deletions;
   Part* parts;
   ccka_totals* out;
+  long long* ovf;  // set when a fixed-point sum would leave int64
   int64_t N;
 };
 
-constexpr int kPartBytes = 10 * 8;
+constexpr int kPartBytes = 11 * 8;
 
 // kernel instantiation chosen for (D, max_nodes): DMAX x MAXN
 inline void kernel_dims(int D, int maxn, int* dmax, int* nmax) {
@@ -293,7 +294,8 @@ struct PgSampleParams {
   int16_t* rec_target;   // nullable [n]
   double* rec_cw;        // nullable [n]
   int64_t n, first_id;
-  uint64_t seed;
+  const uint64_t* seed;  // device word: the Philox key (read at run time, so a
+                         // captured loop replays with any seed)
   int32_t t, _pad;
 };
 hipError_t launch_policy_sample(const PgSampleParams& q, hipStream_t s);

@@ -154,8 +154,9 @@ __global__ void __launch_bounds__(256) policy_sample_kernel(PgSampleParams q) {
     sum += p[a];
   }
   const int64_t g = q.first_id + i;
+  const uint64_t seed = *q.seed;
   uint32_t u4[4];
-  philox((uint32_t)g, (uint32_t)(g >> 32), (uint32_t)q.t, 0x5A3B1E7u, (uint32_t)q.seed, (uint32_t)(q.seed >> 32), u4);
+  philox((uint32_t)g, (uint32_t)(g >> 32), (uint32_t)q.t, 0x5A3B1E7u, (uint32_t)seed, (uint32_t)(seed >> 32), u4);
   const float u = (float)(u4[0] >> 8) * (1.0f / 16777216.0f) * sum;
   int act = MLP_OUT - 1;  // the last action when rounding leaves u above every partial sum
   float acc = 0.f;

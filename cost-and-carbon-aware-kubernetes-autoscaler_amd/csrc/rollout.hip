@@ -2097,35 +2097,53 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
 // Totals: fixed-order block partials, then one ordered final pass.
 // ---------------------------------------------------------------------------
 struct Part {
-  long long v[10];  // ccka_totals' int64 block (energy and gCO2 in fixed point)
+  long long v[11];  // ccka_totals' int64 block (energy and gCO2 in fixed point) + overflow flag
 };
+
+// a + b into a, setting the flag instead of wrapping (signed int64)
+__device__ __forceinline__ void add_chk(long long& a, long long b, long long& ovf) {
+  long long r;
+  if (__builtin_add_overflow(a, b, &r)) ovf = 1;
+  a = r;
+}
+// llrint(x * scale), flagged when it is not representable (|x * scale| >= 2^63)
+__device__ __forceinline__ long long fix_chk(double x, double scale, long long& ovf) {
+  const double y = x * scale;
+  if (!(y > -9.2233720368547758e18 && y < 9.2233720368547758e18)) {
+    ovf = 1;
+    return 0;
+  }
+  return __double2ll_rn(y);
+}
 
 __global__ void __launch_bounds__(256) totals_partial(TotParams q) {
   __shared__ Part sp[256];
   const int tid = threadIdx.x;
   Part a;
 #pragma unroll
-  for (int k = 0; k < 10; ++k) a.v[k] = 0;
+  for (int k = 0; k < 11; ++k) a.v[k] = 0;
+  long long& ovf = a.v[10];
   const int64_t chunk = (q.N + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(lo + chunk, q.N);
   for (int64_t i = lo + tid; i < hi; i += blockDim.x) {
     a.v[0] += 1;
-    a.v[1] += q.cost[i];
-    a.v[2] += q.slo[i];
-    a.v[3] += q.pend_min[i];
+    add_chk(a.v[1], q.cost[i], ovf);
+    a.v[2] += q.slo[i];  // int32 per scenario: < 2^31 * N, no overflow below N = 2^32
+    add_chk(a.v[3], q.pend_min[i], ovf);
     a.v[4] += q.nmin_spot[i];
     a.v[5] += q.nmin_od[i];
     a.v[6] += q.launches[i];
     a.v[7] += q.deletions[i];
-    a.v[8] += __double2ll_rn(q.energy[i] * 1e9);  // llrint, as ccka_oracle_totals
-    a.v[9] += __double2ll_rn(q.gco2[i] * 1e6);
+    add_chk(a.v[8], fix_chk(q.energy[i], 1e6, ovf), ovf);  // llrint, as ccka_oracle_totals
+    add_chk(a.v[9], fix_chk(q.gco2[i], 1e6, ovf), ovf);
   }
   sp[tid] = a;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (tid < s) {
 #pragma unroll
-      for (int k = 0; k < 10; ++k) sp[tid].v[k] += sp[tid + s].v[k];
+      for (int k = 0; k < 10; ++k) add_chk(sp[tid].v[k], sp[tid + s].v[k], sp[tid].v[10]);
+      sp[tid].v[10] |= sp[tid + s].v[10];
     }
     __syncthreads();
   }
@@ -2135,9 +2153,11 @@ __global__ void __launch_bounds__(256) totals_partial(TotParams q) {
 __global__ void totals_final(TotParams q, int nparts) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Part a;
-  for (int k = 0; k < 10; ++k) a.v[k] = 0;
-  for (int b = 0; b < nparts; ++b)
-    for (int k = 0; k < 10; ++k) a.v[k] += q.parts[b].v[k];
+  for (int k = 0; k < 11; ++k) a.v[k] = 0;
+  for (int b = 0; b < nparts; ++b) {
+    for (int k = 0; k < 10; ++k) add_chk(a.v[k], q.parts[b].v[k], a.v[10]);
+    a.v[10] |= q.parts[b].v[10];
+  }
   ccka_totals* o = q.out;
   o->scenarios = a.v[0];
   o->cost_uphmin = a.v[1];
@@ -2147,10 +2167,11 @@ __global__ void totals_final(TotParams q, int nparts) {
   o->node_min_od = a.v[5];
   o->launches = a.v[6];
   o->deletions = a.v[7];
-  o->energy_nwmin = a.v[8];
+  o->energy_uwmin = a.v[8];
   o->gco2_ug = a.v[9];
-  o->energy_wmin = (double)a.v[8] * 1e-9;
+  o->energy_wmin = (double)a.v[8] * 1e-6;
   o->gco2 = (double)a.v[9] * 1e-6;
+  *q.ovf = a.v[10];
 }
 
 // ---------------------------------------------------------------------------

@@ -317,111 +317,31 @@ __device__ __forceinline__ int rate_limit1(const D1Rule& R, bool up, int cur, co
 // The ring is refilled only when every live lane has consumed the rows it
 // overwrites.
 // ---------------------------------------------------------------------------
-// (build-time overrides for tools/build_variants.py; the shipped build uses the defaults)
-#ifndef D1_RB_V
-#define D1_RB_V 64
-#endif
-#ifndef D1_K_V
-#define D1_K_V 2
-#endif
-#ifndef D1_VMN_V
-#define D1_VMN_V 4
-#endif
-#ifndef D1_LEAN_V
-#define D1_LEAN_V 2
-#endif
-#ifndef D1_S_V
-#define D1_S_V 8
-#endif
-// LEAN 2: 1 = a proposal below cur held by the down window is a quiet step
-// (its record is rebuilt at the next event), 0 = such a step is an event, so
-// every quiet record is cur and the rebuild is a fill (measured: 0 makes 21 %
-// of config 2's lane-steps events, 2x slower)
-#ifndef D1_HELD_V
-#define D1_HELD_V 1
-#endif
-// LEAN 2: quiet steps may cross one clock-hour boundary; the next event step
-// charges the hour that ended and starts the new one (prices, carbon
-// intensity) for them (not with replacement consolidation, whose offers are
-// re-evaluated at every hour)
-#ifndef D1_LAZYH_V
-#define D1_LAZYH_V 0
-#endif
-// price tiles, carbon intensity and J from an LDS copy when they fit (the
-// event step's hour-change reads then wait for no older vector-memory
-// operation: every global load does, the trajectory stores and trace DMAs
-// included)
-#ifndef D1_LDST_V
-#define D1_LDST_V 1
-#endif
-// top-of-iteration wait: with the lean quiet path every iteration issues
-// exactly D1_S record stores after its refill DMAs, and vector-memory
-// operations complete in issue order, so vmcnt(D1_VMN + D1_S) still retires
-// every row but the D1_VMN youngest while leaving the records in flight
-#ifndef D1_WAITS_V
-#define D1_WAITS_V 0
-#endif
-constexpr int D1_RB = D1_RB_V;    // ring rows (power of two)
-constexpr int D1_K = D1_K_V;      // event cadence (iterations)
-constexpr int D1_VMN = D1_VMN_V;  // rows in flight (vmcnt bound; <= 63)
-constexpr int D1_S = D1_S_V;      // quiet steps per iteration and lane
-// rows kept behind the slowest lane: the LEAN 2 event step rebuilds the
-// down-window records of its quiet steps from them (window <= CCKA_HIST steps)
-constexpr int D1_BACK = D1_LEAN_V == 2 ? CCKA_HIST : 0;
+constexpr int D1_RB = 64;   // ring rows (power of two)
+constexpr int D1_K = 2;     // event cadence (iterations)
+constexpr int D1_VMN = 4;   // rows in flight (vmcnt bound; <= 63)
+constexpr int D1_S = 8;     // quiet steps per iteration and lane
+// rows kept behind the slowest lane: the event step rebuilds the down-window
+// records of its quiet steps from them (window <= CCKA_HIST steps)
+constexpr int D1_BACK = CCKA_HIST;
 // the initial fill (D1_VMN + 4 D1_S rows) plus the rows kept behind must fit,
 // and the lanes must be able to spread over a few iterations' worth of rows
 static_assert(D1_VMN + 4 * D1_S + D1_BACK <= D1_RB && D1_RB - D1_S - D1_BACK - D1_VMN >= 2 * D1_S,
               "ring too small for the DMA lead");
 constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
-// packed ring rows: a row holds the wave's lpw scenarios (4 lpw bytes), so
-// the same D1_RING_BYTES hold 4096 / lpw rows (83 at 49 lanes instead of 64)
-// and the lanes may drift further apart before the slowest one blocks the
-// refill (the row count is then a runtime value: rows by modulo, not mask)
-#ifndef D1_PACK_V
-#define D1_PACK_V 0
-#endif
-// x mod n for 0 <= x < 2^17, n <= 4096, rn = 1/(float)n: the f32 quotient is
-// within one of the truth, one correction on each side makes it exact
-__device__ __forceinline__ int d1_mod(int x, int n, float rn) {
-  const int q = (int)((float)x * rn);
-  int r = x - q * n;
-  r += r < 0 ? n : 0;
-  r -= r >= n ? n : 0;
-  return r;
-}
-
-// streaming hint on the trace rows (build variant)
-#ifndef D1_NTL_V
-#define D1_NTL_V 0
-#endif
-#if D1_NTL_V
-#define D1_NTL " nt"
-#else
-#define D1_NTL ""
-#endif
 // Trajectory records go through a buffer resource over the wave's [lanes][T]
 // record block: the hardware drops a store whose offset lies past num_records,
 // so an out-of-range offset masks a lane's store without an exec-mask branch,
 // and num_records = 0 turns every store off when no trajectory is kept.
 constexpr int D1_NOSTORE = 0x7FFFFFF0;
-// wave priority: 1 = raised during event runs, 2 = raised outside them (quiet
-// steps and the loop). Every variant measured 4 % faster than none, whatever
-// the level and direction (tools/variant_bench.py: 1.815-1.827 vs 1.904 ms),
-// so the gain is as much the s_setprio boundaries as the arbitration
-#ifndef D1_PRIO_V
-#define D1_PRIO_V 2
-#endif
-#ifndef D1_PRIO_HI
-#define D1_PRIO_HI 3
-#endif
-// cache policy of the record stores (build variant: 2 = nt, streaming)
-#ifndef D1_NTS_V
-#define D1_NTS_V 0
-#endif
+// wave priority raised outside the event runs (quiet steps and the loop): 4 %
+// faster than none in round 3, whatever the level and direction (the gain is
+// as much the s_setprio boundaries as the arbitration)
+constexpr int D1_PRIO_HI = 3;
 __device__ __forceinline__ void d1_store_rec(__amdgpu_buffer_rsrc_t r, int voff, const int4& v) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   const i32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, D1_NTS_V);
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, 0);
 }
 
 __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row) {
@@ -430,17 +350,13 @@ __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row)
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, off" D1_NTL "\n\t"
+      "global_load_lds_dword %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(src), "s"(lds_row)
       : "memory");
 }
-template <bool LEAN>
-__device__ __forceinline__ void d1_wait_rows() {
-  if constexpr (LEAN && D1_WAITS_V) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN + D1_S) : "memory");
-  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN) : "memory");
-}
+__device__ __forceinline__ void d1_wait_rows() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN) : "memory"); }
 __device__ __forceinline__ void d1_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Argmin-table reads of the event step through the scalar data cache: a
@@ -449,42 +365,34 @@ __device__ __forceinline__ void d1_wait_all() { asm volatile("s_waitcnt vmcnt(0)
 // issue order), a scalar load only for older scalar ones. The active lanes'
 // addresses are taken four at a time (v_readlane), loaded with s_load_dwordx2
 // and handed back to their lanes.
-#ifndef D1_SLD_V
-#define D1_SLD_V 1
-#endif
 #define CONST_AS __attribute__((address_space(4)))
 __device__ __forceinline__ int2 d1_tload(const GLOBAL_AS int2* ptr) {
-  if constexpr (!D1_SLD_V) {
-    const uint64_t v = *(const GLOBAL_AS uint64_t*)ptr;
-    return make_int2((int)(uint32_t)v, (int)(uint32_t)(v >> 32));
-  } else {
-    const uint64_t a = (uint64_t)ptr;
-    const int alo = (int)(uint32_t)a, ahi = (int)(uint32_t)(a >> 32);
-    const int me = (int)(threadIdx.x & (WAVE - 1));
-    uint64_t m = __ballot(1);
-    int ox = 0, oy = 0;
-    while (m) {
-      int l[4];
+  const uint64_t a = (uint64_t)ptr;
+  const int alo = (int)(uint32_t)a, ahi = (int)(uint32_t)(a >> 32);
+  const int me = (int)(threadIdx.x & (WAVE - 1));
+  uint64_t m = __ballot(1);
+  int ox = 0, oy = 0;
+  while (m) {
+    int l[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        l[k] = m ? __ffsll((long long)m) - 1 : l[0];
-        m &= m - 1;  // (0 stays 0)
-      }
-      uint64_t v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t ak = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(alo, l[k]) |
-                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane(ahi, l[k]) << 32;
-        v[k] = *(const CONST_AS uint64_t*)ak;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        ox = me == l[k] ? (int)(uint32_t)v[k] : ox;
-        oy = me == l[k] ? (int)(uint32_t)(v[k] >> 32) : oy;
-      }
+    for (int k = 0; k < 4; ++k) {
+      l[k] = m ? __ffsll((long long)m) - 1 : l[0];
+      m &= m - 1;  // (0 stays 0)
     }
-    return make_int2(ox, oy);
+    uint64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t ak = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(alo, l[k]) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane(ahi, l[k]) << 32;
+      v[k] = *(const CONST_AS uint64_t*)ak;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ox = me == l[k] ? (int)(uint32_t)v[k] : ox;
+      oy = me == l[k] ? (int)(uint32_t)(v[k] >> 32) : oy;
+    }
   }
+  return make_int2(ox, oy);
 }
 
 // logical block of dispatch block b among n (a bijection; 8 XCDs)
@@ -504,7 +412,7 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1, int HE = 8,
           bool G3 = false>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
-  static_assert(NSUB == 1 || (NSUB == 4 && BDEF && D1_LEAN_V == 2 && D1_HELD_V), "15 s sync: lean default path");
+  static_assert(NSUB == 1 || (NSUB == 4 && BDEF), "15 s sync: lean default path");
   static_assert(HE == 8 || (HE == 4 && NSUB == 1 && BDEF), "4-record ring: default behavior, one decision per step");
   constexpr int HW = NSUB == 1 ? HE / 2 : 10;  // history words (2 records each)
   // steps whose records the event step may rebuild: the window's entries
@@ -520,7 +428,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   }
   // LDS copies of the price tiles [R][24][K][Z][2], ci [R][24] and J
   // [R][24][NZI][3] after the rings (launch_rollout_d1 sets lds_tab when they fit)
-  const bool ldt = D1_LDST_V && p.lds_tab;
+  const bool ldt = p.lds_tab;
   const uint32_t tab_off = ((uint32_t)p.K * 16u + 255u) / 256u * 256u + (blockDim.x / WAVE) * (uint32_t)D1_RING_BYTES;
   const int n_pr = p.R * 24 * p.K * p.Z * 2;
   const int n_pr8 = (n_pr + 1) & ~1;
@@ -686,12 +594,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   float Rmax = 0.f;             // max over ready slots of pods/alloc
   float q_rbd = 0.f, q_rbc = 0.f, q_rbp = 0.f;  // 1/(ready*req), 1/(cur*req), 1/ready pods
   bool q_peak = false;
-  int q_rcap = 0, q_dreq = 1, q_dcur = 1;  // usage cap (ready*limit, or INT_MAX without a limit), ready*req, cur*req
-  int q_mode = 2;               // 0: metric (ready*req < 2^24), 1: no metric and replicas in range, 2: events only
-  bool q_unr = false;           // unready pods
+  int q_rcap = 0;               // usage cap (ready*limit, or INT_MAX without a limit)
   int q_hold = -0x40000000;     // the down window holds a record >= cur up to this step
-  bool q_atmax = false, q_pend = false;  // cur >= maxReplicas, pending pods
-  int q_umax = -1;  // largest usage the quiet step evaluates exactly (-1: every step is an event)
   (void)dnmask;
   // steps a record >= cur holds the replica count for (every decision of a
   // later step must see it: (nd - (NSUB - 1)) / NSUB whole steps), and the
@@ -713,14 +617,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int q_ulim = 0, q_pge = 0, q_slo = 0, q_usat = 0, q_w0 = 0, q_w1 = 0, q_pendv = 0, q_nodes = 0;
   float q_hbp = 0.f;   // 0.5 / ready pods (upp = (usage + 0.5) / ready pods, truncated)
   uint32_t usum = 0;   // sum of upp over the quiet steps since the last flush
-  // lazy hour crossing: th = the next clock-hour boundary step; quiet steps at
-  // or after it add their upp to usumB too (and a saturation correction to
-  // ecB); lazy_n2 (> 0 after a crossing) steps of node cost wait for the new
-  // hour's prices
-  constexpr bool LAZY_OK = BDEF && D1_LEAN_V == 2 && D1_LAZYH_V;
-  int th = 0x7fffffff, lazy_n2 = 0;
-  uint32_t usumB = 0;
-  long long ecB = 0;
   bool q_met = false;  // the HPA has a metric (records are proposals, else invalid)
 
   auto refresh_J = [&](int rh) {
@@ -871,29 +767,11 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // per-step constants of the quiet steps since the last event (SEMANTICS §3.H)
   auto flush = [&](int upto) {
     const int n = upto - tq;
-    if (LAZY_OK && th < upto) {
-      // the quiet steps crossed the hour boundary th: charge [tq, th) to the
-      // hour that ended (its carbon intensity is still loaded), start the new
-      // hour's energy with [th, upto); their node cost follows the reload of
-      // the new hour's prices (hchg)
-      const int n1 = th - tq, n2 = upto - th;
-      cost += (burn + base_price) * (long long)n1;
-      e_hour += (base_nw + Isum) * (long long)n1 + (long long)(Ssum * (unsigned long long)(usum - usumB));
-      gco2 += (double)e_hour * (ci_min * 1e-9);
-      energy_nw += e_hour;
-      e_hour = (base_nw + Isum) * (long long)n2 + (long long)(Ssum * (unsigned long long)usumB) + ecB;
-      hour = ((sm0 + th) % 1440) / 60;
-      lazy_n2 = n2;  // >= 1: also the "crossed" flag until the reload
+    cost += (burn + base_price) * (long long)n;
+    e_hour += (base_nw + Isum) * (long long)n;
+    if constexpr (BDEF) {  // dynamic energy of the quiet steps (exact integers)
+      e_hour += (long long)(Ssum * (unsigned long long)usum);
       usum = 0;
-      usumB = 0;
-      ecB = 0;
-    } else {
-      cost += (burn + base_price) * (long long)n;
-      e_hour += (base_nw + Isum) * (long long)n;
-      if constexpr (BDEF && D1_LEAN_V == 2) {  // dynamic energy of the quiet steps (exact integers)
-        e_hour += (long long)(Ssum * (unsigned long long)usum);
-        usum = 0;
-      }
     }
     pend_min += (replicas - rpods) * n;
     nmin_spot += nsp * n;
@@ -911,14 +789,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const uint32_t ring_lds = (uint32_t)(uintptr_t)s_acc + ring_off;
   const int* const ring = reinterpret_cast<const int*>(reinterpret_cast<const char*>(s_acc) + ring_off);
   // ring geometry (wave-uniform): rbn rows of rsw lanes; row of step x = x mod rbn
-  const int rsw = D1_PACK_V ? opq(p.lpw) : WAVE;
-  const int rbn = D1_PACK_V ? min(D1_RING_BYTES / (4 * rsw), 4096) : D1_RB;
-  const float rrbn = D1_PACK_V ? 1.0f / (float)rbn : 0.f;
-  auto rrow = [&](int x) { return D1_PACK_V ? d1_mod(x, rbn, rrbn) : (x & (D1_RB - 1)); };
+  constexpr int rsw = WAVE, rbn = D1_RB;
+  auto rrow = [&](int x) { return x & (D1_RB - 1); };
   // ring index of (row r, this lane)
   auto ridx = [&](int r) { return r * rsw + lane; };
   // row r + q (0 <= q < rbn) wrapped
-  auto rnext = [&](int r, int q) { return D1_PACK_V ? (r + q >= rbn ? r + q - rbn : r + q) : ((r + q) & (D1_RB - 1)); };
+  auto rnext = [&](int r, int q) { return (r + q) & (D1_RB - 1); };
   int tf = 0;   // trace rows issued (wave-uniform)
   int tfr = 0;  // tf mod rbn (wave-uniform)
   const int32_t* lpf = lp;  // this lane's sample of row tf
@@ -960,7 +836,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   for (int it = 0;; ++it) {
     const bool live = t < T;
     if (__ballot(live) == 0) break;  // wave-uniform
-    d1_wait_rows<BDEF && D1_LEAN_V == 2>();
+    d1_wait_rows();
     t_rdy = max(t_rdy, tf - D1_VMN);
     // ---- event steps of the stalled lanes: every D1_K iterations, or when no
     // lane stepped quietly in the last one. They run before this iteration's
@@ -970,8 +846,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     const uint64_t sb = __ballot(stall);
     if constexpr (STAMPS) st_acc[9] += 1;
     if (sb != 0 && (it % D1_K == D1_K - 1 || !qadv)) {
-      if constexpr (D1_PRIO_V == 1) __builtin_amdgcn_s_setprio(D1_PRIO_HI);
-      if constexpr (D1_PRIO_V == 2) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       if constexpr (STAMPS) { st_acc[10] += 1; st_acc[11] += __popcll(sb); }
       // the event step in phases, each a block over the stalled lanes (the
       // wave-uniform points between them carry the diagnostic stamps)
@@ -986,26 +861,14 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         stall = false;
         const int tr = rrow(t);
         L = ring[ridx(tr)];
-        if constexpr (BDEF && D1_LEAN_V == 2) {
+        if constexpr (BDEF) {
           // the down-window records of the quiet steps [tq, t), oldest first,
           // from their trace rows (the ring keeps >= 8 rows behind every lane)
           // and the state they ran with. A record >= cur is stored as cur: the
           // default behavior only ever compares it with a proposal and with cur
           // (<= maxReplicas), so its excess over cur never changes a decision.
           const int kq = min(t - tq, wr);
-          if constexpr (!D1_HELD_V) {
-            // every quiet record is cur (or invalid without a metric)
-            const int rv = q_met ? min(replicas, D1_REC_SAT) : (int)0x8000;
-            const uint32_t rr = ((uint32_t)rv & 0xFFFFu) * 0x10001u;
-            if (kq >= wl) {  // the whole window is quiet steps (entries >= wl are never read)
-#pragma unroll
-              for (int w = 0; w < HW; ++w) hdn[w] = rr;
-            } else {
-#pragma unroll
-              for (int j = 1; j < CCKA_HIST; ++j)
-                if (j <= kq) ring_push<HW>(hdn, rv);
-            }
-          } else if (kq > 0) {
+          if (kq > 0) {
             // entry j of the rebuilt window = the record of step t-1-j (j < kq);
             // the rows' samples are read first (independent LDS reads), held
             // proposals are computed only in waves where some lane has one
@@ -1054,7 +917,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           }
         }
         flush(t);
-        if (LAZY_OK && lazy_n2 > 0) hchg = true;  // quiet steps crossed into this hour: load its prices below
         minute = (sm0 + t) % 1440;
         const int h = minute / 60;
         rh = r * 24 + h;
@@ -1213,10 +1075,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               sprice[n] = np[n];
               burn += np[n];
             }
-          }
-          if constexpr (LAZY_OK) {  // node cost of the quiet steps since the lazy crossing
-            cost += (burn + base_price) * (long long)lazy_n2;
-            lazy_n2 = 0;
           }
         }
         if (hchg || jchg) refresh_J(rh);
@@ -1867,7 +1725,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                         (step_last_type & 0xFFFF) | (int)(flags << 16));
 
         // ---- caches of the quiet steps that follow ----
-        if constexpr (BDEF && D1_LEAN_V == 2) {
+        if constexpr (BDEF) {
           constexpr int UQ = 1 << 20;  // quiet usages: [0, 2^20)
           // smallest usage with floor(100 * usage / d) >= u (u >= 0), capped at UQ
           auto umin = [](int u, uint32_t d) -> int {
@@ -1934,33 +1792,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         } else {
           q_rbd = __builtin_amdgcn_rcpf((float)(rpods * req));
           q_rbc = __builtin_amdgcn_rcpf((float)(replicas * req));
-          // (rpods, replicas <= 32767 and req, limit <= 65535: exact 24-bit products)
-          q_rcap = limit > 0 ? (int)__umul24((uint32_t)rpods, (uint32_t)limit) : 0x7fffffff;
-          q_dreq = (int)__umul24((uint32_t)rpods, (uint32_t)req);
-          q_dcur = (int)__umul24((uint32_t)replicas, (uint32_t)req);
-          {
-            const bool met = replicas <= mx && replicas >= minr && rpods > 0 && !(replicas == 0 && minr != 0);
-            const bool hpa_path = !(replicas == 0 && minr != 0);
-            const int dnm = replicas > mx ? mx : (replicas < minr && hpa_path ? minr : replicas);
-            q_mode = met ? (q_dreq < (1 << 24) ? 0 : 2) : (dnm == replicas ? 1 : 2);
-          }
-          q_unr = replicas > rpods;
-          q_atmax = replicas >= mx;
-          q_pend = replicas > rpods;
-          // Exactness range of the quiet step's arithmetic: usage < 2^20 (f32
-          // exact), util < 2^16 (usage*100 < 2^16*ready*req), and proposal
-          // estimates u*base/target < 2^20 for u < 2^16 (base < 16*target), so
-          // every f32 quotient is within one of the truth and one remainder
-          // correction makes it exact. Outside it, or in mode 2, every step
-          // is an event (the general evaluation is exact everywhere).
-          {
-            // usage*100 < 2^16*dreq, from below: 655.35 < 2^16/100 and f32 rounding
-            // (< 2^-23 relative) cannot reach the 1.5e-5 margin
-            const int ucap = (int)fminf((float)q_dreq * 655.35f, 1048575.0f);
-            const int base_max = q_unr ? max(replicas, rpods) : rpods;
-            const bool ok = q_mode < 2 && base_max < 16 * target && (!q_unr || q_dcur < (1 << 24));
-            q_umax = !ok ? -1 : (q_mode == 1 ? 0x7fffffff : ucap);
-          }
         }
         if constexpr (BDEF) {  // newest history record >= the new replica count
           int hit = -0x40000000;
@@ -1970,8 +1801,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             hit = e >= replicas ? t - k / NSUB : hit;
           }
           q_hold = replicas <= minr ? 0x3fffffff : hit + wl;
-          // LEAN 2 without a metric: no records, nothing to hold
-          if (D1_LEAN_V == 2 && !q_met) q_hold = 0x3fffffff;
+          // without a metric: no records, nothing to hold
+          if (!q_met) q_hold = 0x3fffffff;
         }
         // first step that needs the event path again: a node becomes ready,
         // an hour or peak-window boundary, a slot becomes a consolidation
@@ -1980,10 +1811,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // with the same candidates), or the next step when disruption acted
         // (the budget may allow more)
         {
-          th = t + 60 - minute % 60;  // the next clock-hour boundary
-          // lazy: quiet steps may cross it, but the event that charges the
-          // crossing must fall inside the new hour (its prices load there)
-          int nx = min(next_ready, (LAZY_OK && !(DRIFT && replace)) ? th + 59 : th);
+          const int th = t + 60 - minute % 60;  // the next clock-hour boundary
+          int nx = min(next_ready, th);
           if (pswitch) {
             if (t >= npb) {  // the next peak-window boundary
               const int dps = (ps - minute + 1439) % 1440 + 1, dpe = (pe - minute + 1439) % 1440 + 1;
@@ -2009,8 +1838,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       pf_ok = pf_ok && !ev;
       D1_STAMP(7);
     }
-    if constexpr (D1_PRIO_V == 1) __builtin_amdgcn_s_setprio(0);
-    if constexpr (D1_PRIO_V == 2) __builtin_amdgcn_s_setprio(D1_PRIO_HI);
+    __builtin_amdgcn_s_setprio(D1_PRIO_HI);
     // ---- ring refill: D1_S rows per iteration once every lane has consumed
     // what they overwrite; issued after the event steps, whose own loads
     // wait for every older vector-memory operation ----
@@ -2039,26 +1867,24 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     const int tlim = min(T, t_rdy);
 #pragma unroll
     for (int sub = 0; sub < D1_S; ++sub) {
-    if constexpr (BDEF && D1_LEAN_V == 2) {
+    if constexpr (BDEF) {
         const int L = Lpf[sub];
         // two usage compares decide the HPA (see q_ulim / q_pge); the rest is
         // accounting, the SLO test and the trajectory record, all predicated
         // on `go` (no branch but the rare saturation one)
         const int usage = min(L, q_rcap);
         const bool ge = usage >= q_pge;
-        const bool ok = (t < nxt) & ((uint32_t)usage < (uint32_t)q_ulim) & (ge | (D1_HELD_V && t <= q_hold));
+        const bool ok = (t < nxt) & ((uint32_t)usage < (uint32_t)q_ulim) & (ge | (t <= q_hold));
         const bool can = !stall & (t < tlim);
         const bool go = ok & can;
         stall = stall | (can & !ok);
-        if constexpr (D1_HELD_V) q_hold = (go & ge) ? max(q_hold, t + wl) : q_hold;
+        q_hold = (go & ge) ? max(q_hold, t + wl) : q_hold;
         const int upp = (int)fmaf((float)usage, q_rbp, q_hbp);
         if (__builtin_expect(go & (upp > q_usat), 0)) {  // a node may saturate: exact per-node sum instead
           const long long corr = dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-          if (LAZY_OK && t >= th) ecB += corr;
-          else e_hour += corr;
+          e_hour += corr;
         }
         usum += go ? (uint32_t)upp : 0u;
-        if constexpr (LAZY_OK) usumB += (go & (t >= th)) ? (uint32_t)upp : 0u;
         const bool slo_b = usage >= q_slo;
         slo += (go & slo_b) ? 1 : 0;
         d1_store_rec(trs, go ? lb + t * 16 : D1_NOSTORE, make_int4(replicas, q_pendv, q_nodes, slo_b ? q_w1 : q_w0));
@@ -2069,72 +1895,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       // a lane still stepping in sub-step `sub` has advanced in every earlier one
       const int L = Lpf[sub];
       int4 rec;
-      if constexpr (BDEF && D1_LEAN_V == 1) {
-        // Upstream default behavior, decided without the general path:
-        // keep (util inside the tolerance band) leaves the replicas; a
-        // proposal above cur changes nothing at maxReplicas; one below cur
-        // changes nothing while the down window holds a record >= cur
-        // (q_hit) or at minReplicas. util and the proposal ceil(u*ready/target)
-        // are f32-reciprocal divisions with exact remainder corrections on
-        // 24-bit products; anything outside their exact range, the unready
-        // rule, an exact-multiple proposal (binary64 in the spec) or any
-        // replica change is an event.
-        {
-          const int cur = replicas;
-          const int usage = min(L, q_rcap);
-          const int a = (int)__umul24((uint32_t)usage, 100u);
-          int util = (int)((float)a * q_rbd);
-          const int ra = a - (int)__umul24((uint32_t)util, (uint32_t)q_dreq);
-          util += (ra >= q_dreq ? 1 : 0) - (ra < 0 ? 1 : 0);
-          // unready pods and util above target: every replica counted, unready ones idle
-          const bool unr_up = q_unr & (util > target);
-          int u = util, base = rpods;
-          if (unr_up) {
-            int nu = (int)((float)a * q_rbc);
-            const int rn = a - (int)__umul24((uint32_t)nu, (uint32_t)q_dcur);
-            nu += (rn >= q_dcur ? 1 : 0) - (rn < 0 ? 1 : 0);
-            u = nu;
-            base = cur;
-          }
-          const bool keep = ((uint32_t)(u - ulo) <= (uint32_t)(uhi - ulo)) | (unr_up & (u < target));
-          const int x = (int)__umul24((uint32_t)u, (uint32_t)base);
-          int c = (int)((float)x * rtarget);
-          int rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
-          c += (rc >= target ? 1 : 0) - (rc < 0 ? 1 : 0);
-          rc = x - (int)__umul24((uint32_t)c, (uint32_t)target);
-          const bool met = q_mode == 0;  // else 1: no metric, replicas in range (an invalid record)
-          // usage <= q_umax proves every estimate above exact (see the caches)
-          const bool bad = (uint32_t)usage > (uint32_t)q_umax;
-          c += rc != 0 ? 1 : 0;
-          if (__builtin_expect(met & !bad & !keep & (rc == 0), 0))  // binary64 as the spec writes it
-            c = (int)ceil(((double)u / (double)target) * (double)base);
-          const int pr = (met & !keep) ? (unr_up ? max(cur, c) : c) : cur;
-          // above cur: held at maxReplicas; below: held while the down window
-          // has a record >= cur (q_hold, unbounded at minReplicas)
-          const bool hold = ((pr <= cur) | q_atmax) & ((pr >= cur) | (t <= q_hold));
-          // the step's energy: independent of the HPA chain above (interleaves with it)
-          int upp = (int)((float)usage * q_rbp);
-          const int ru = usage - (int)__umul24((uint32_t)upp, (uint32_t)rpods);
-          upp += (ru >= rpods ? 1 : 0) - (ru < 0 ? 1 : 0);
-          const bool sat = !((float)upp * Rmax < 0.9999f);
-          const long long edq = (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-          stall = (t >= nxt) | bad | !hold;
-          if (!stall) {
-            ring_push(hdn, met ? min(pr, D1_REC_SAT) : (int)0x8000);
-            q_hold = (met & (pr >= cur)) ? max(q_hold, t + wl) : q_hold;
-            long long ed = edq;
-            if (__builtin_expect(sat, 0)) ed = dyn_energy(upp);  // a node saturates
-            e_hour += ed;
-            const bool slo_b = q_pend | (met & (util > slo_util));
-            slo += slo_b ? 1 : 0;
-            rec = make_int4(cur, cur - rpods, (nsp & 0xFFFF) | nod << 16,
-                            0xFFFF | (int)((q_peak ? 1u : 0u) << 16) | (slo_b ? (8 << 16) : 0));
-            adv = true;
-            d1_store_rec(trs, lb + t * 16, rec);
-            ++t;
-          }
-        }
-      } else if (!(stall = t >= nxt)) {
+      if (!(stall = t >= nxt)) {
         const HpaOut h = hpa_eval(L, replicas, rpods, q_rbd, q_rbc);
         stall = h.desired != replicas;
         if (!stall) {
@@ -2174,18 +1935,6 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     }
   }
   flush(T);
-  if (LAZY_OK && lazy_n2 > 0) {  // the last quiet steps crossed into a new hour: its prices and carbon intensity
-    const int rh = r * 24 + hour;
-    const GLOBAL_AS int32_t* tile = price + (int64_t)rh * K * Z * 2;
-    ci_min = ci_gpwmin[rh];
-    long long b = (long long)base_nodes * tile[(base_type * Z) * 2 + 1];
-#pragma unroll
-    for (int n = 0; n < MAXN; ++n) {
-      const uint32_t x = sinfo[n];
-      if (used >> n & 1u) b += tile[((int)(x & 1023u) * Z + (int)(x >> 10 & 3u)) * 2 + (int)(x >> 12 & 1u)];
-    }
-    cost += b * (long long)lazy_n2;
-  }
   energy_nw += e_hour;
   gco2 += (double)e_hour * (ci_min * 1e-9);
   p.cost[i] = cost;
@@ -2254,7 +2003,7 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   const size_t tabB = ((npr + 1) & ~(size_t)1) * 4 + (size_t)p.R * 24 * 8 + (size_t)p.R * 24 * p.NZI * 3 * 4;
   D1Params q = p;
   q.lds_tab = 0;
-  if (D1_LDST_V && lds + tabB <= 80 * 1024) {
+  if (lds + tabB <= 80 * 1024) {
     q.lds_tab = 1;
     lds += tabB;
   }

@@ -87,7 +87,7 @@ static int run_world(ccka_host* h) {
   std::vector<ccka_detail> det((size_t)n);
   if (ccka_oracle_rollout_detail(&w, &sc, load.data(), &r, traj.data(), det.data(), 2) != CCKA_OK) return 4;
   ccka_totals tot;
-  ccka_oracle_totals(&r, n, &tot);
+  if (ccka_oracle_totals(&r, n, &tot) != CCKA_OK) return 8;
   if (ccka_host_summary(h, &w, &r, traj.data(), det.data(), buf.data(), (int64_t)buf.size()) < 0) return 5;
   if (ccka_host_summary(h, &w, &r, nullptr, nullptr, buf.data(), (int64_t)buf.size()) < 0) return 5;
   int64_t need = 0;

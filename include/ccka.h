@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define CCKA_ABI_VERSION 4
+#define CCKA_ABI_VERSION 5
 
 #define CCKA_STEP_SECONDS 60
 #define CCKA_MAX_TYPES 1024
@@ -54,7 +54,8 @@ enum ccka_status {
   CCKA_ERCCL = -4,    /* RCCL error */
   CCKA_EPARITY = -5,  /* self-check mismatch */
   CCKA_ESTATE = -6,   /* call order (e.g. rollout before set_world) */
-  CCKA_ENODEV = -7    /* no usable gfx950 device */
+  CCKA_ENODEV = -7,   /* no usable gfx950 device */
+  CCKA_EOVERFLOW = -8 /* a fixed-point total would leave int64 (ccka_totals) */
 };
 
 /* capacity-type bits (karpenter.sh/capacity-type); offering index c: 0 spot, 1 on-demand */
@@ -269,7 +270,13 @@ typedef struct ccka_traj_rec {
  * tree and the rank count: energy and gCO2 are summed in fixed point, each
  * scenario's value rounded once (llrint: to nearest, ties to even). The two
  * doubles are derived from them after every sum (ccka_get_totals,
- * ccka_allreduce_totals), so they too are bit-identical at any rank count. */
+ * ccka_totals_finish), so they too are bit-identical at any rank count.
+ * Units and headroom: energy in microwatt-minutes (a config-3 scenario, one
+ * day on up to 8 nodes, is ~8.6e9 uW.min, so int64 holds ~1e9 such scenarios
+ * summed over all ranks), gCO2 in micrograms (~5.7e10 ug per such scenario at
+ * 400 g/kWh: ~1.6e8 scenarios). A sum that would leave int64 is reported as
+ * CCKA_EOVERFLOW (ccka_get_totals, ccka_totals_finish,
+ * ccka_allreduce_totals), never wrapped. */
 typedef struct ccka_totals {
   int64_t scenarios;
   int64_t cost_uphmin;
@@ -279,12 +286,15 @@ typedef struct ccka_totals {
   int64_t node_min_od;
   int64_t launches;
   int64_t deletions;
-  int64_t energy_nwmin;         /* sum of llrint(energy_wmin[i] * 1e9): nanowatt-minutes */
-  int64_t gco2_ug;              /* sum of llrint(gco2[i] * 1e6): micrograms              */
-  double energy_wmin;           /* energy_nwmin * 1e-9 */
+  int64_t energy_uwmin;         /* sum of llrint(energy_wmin[i] * 1e6): microwatt-minutes */
+  int64_t gco2_ug;              /* sum of llrint(gco2[i] * 1e6): micrograms               */
+  double energy_wmin;           /* energy_uwmin * 1e-6 */
   double gco2;                  /* gco2_ug * 1e-6      */
 } ccka_totals;
-#define CCKA_TOTALS_INT64 10    /* leading int64 fields: the all-reduced block */
+#define CCKA_TOTALS_INT64 10    /* leading int64 fields of ccka_totals */
+/* The exchanged block: the CCKA_TOTALS_INT64 fields plus one overflow guard
+ * word (the count of ranks whose own values could make the sum leave int64). */
+#define CCKA_TOTALS_BLOCK 11
 
 /* Per-grid sums of a policy sweep (BASELINE config 4): grid g = the scenarios
  * with global ids [g*grid_size, (g+1)*grid_size). 48 bytes. */
@@ -457,13 +467,24 @@ int ccka_mlp_backward(ccka_ctx* ctx, const uint16_t* x, const uint8_t* actions, 
 /* Fill a 128-byte RCCL unique id (rank 0 only; distribute it out of band). */
 int ccka_comm_unique_id(uint8_t* id128);
 int ccka_comm_init(ccka_ctx* ctx, const uint8_t* id128, int32_t nranks, int32_t rank);
-/* In-place sum of the packed totals across ranks: one RCCL all-reduce of the
- * CCKA_TOTALS_INT64 int64 fields, then energy_wmin / gco2 re-derived from
- * them (bit-identical at any rank count). */
+/* In-place sum of the packed totals across ranks: ccka_totals_pack, one RCCL
+ * all-reduce (sum) of the CCKA_TOTALS_BLOCK int64 words, ccka_totals_finish
+ * (bit-identical at any rank count; CCKA_EOVERFLOW on every rank when the
+ * sum could leave int64). */
 int ccka_allreduce_totals(ccka_ctx* ctx, ccka_totals* inout);
 /* Rank count and this context's rank as the RCCL communicator reports them
  * (ncclCommCount / ncclCommUserRank); CCKA_ESTATE without ccka_comm_init. */
 int ccka_comm_info(ccka_ctx* ctx, int32_t* nranks, int32_t* rank);
+
+/* Host-side halves of the totals exchange (no context, no GPU): the block
+ * a rank contributes to the sum, and the totals of a summed block. A rank
+ * whose fields exceed INT64_MAX / nranks in magnitude sets the guard word, so
+ * after the sum every rank sees the same guard and ccka_totals_finish returns
+ * CCKA_EOVERFLOW on all of them (no rank leaves the collective early). Any
+ * transport that sums int64 words (RCCL here, gloo in the CPU tests) can carry
+ * the block. n must be CCKA_TOTALS_BLOCK. */
+int ccka_totals_pack(const ccka_totals* in, int32_t nranks, int64_t* block, int32_t n);
+int ccka_totals_finish(const int64_t* block, int32_t n, ccka_totals* out);
 
 /* ---- introspection ---------------------------------------------------- */
 /* Name and compute-unit count of the context's device. */

@@ -1392,20 +1392,39 @@ int ccka_oracle_rollout_policy(const ccka_world* w, const ccka_scenarios* sc, co
   return CCKA_OK;
 }
 
-void ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* o) {
+/* a += b, flagging instead of wrapping */
+static void o_add(int64_t* a, int64_t b, int* ovf) {
+  int64_t r;
+  if (__builtin_add_overflow(*a, b, &r)) *ovf = 1;
+  *a = r;
+}
+/* llrint(x * scale), flagged when not representable */
+static int64_t o_fix(double x, double scale, int* ovf) {
+  const double y = x * scale;
+  if (!(y > -9.2233720368547758e18 && y < 9.2233720368547758e18)) {
+    *ovf = 1;
+    return 0;
+  }
+  return llrint(y);
+}
+
+int ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* o) {
+  int ovf = 0;
   memset(o, 0, sizeof *o);
   o->scenarios = n;
   for (int64_t i = 0; i < n; ++i) {
-    o->cost_uphmin += r->cost_uphmin[i];
-    o->slo_minutes += r->slo_minutes[i];
-    o->pending_pod_minutes += r->pending_pod_minutes[i];
-    o->node_min_spot += r->node_min_spot[i];
-    o->node_min_od += r->node_min_od[i];
-    o->launches += r->launches[i];
-    o->deletions += r->deletions[i];
-    o->energy_nwmin += llrint(r->energy_wmin[i] * 1e9);  /* fixed point, as the device totals */
-    o->gco2_ug += llrint(r->gco2[i] * 1e6);
+    o_add(&o->cost_uphmin, r->cost_uphmin[i], &ovf);
+    o_add(&o->slo_minutes, r->slo_minutes[i], &ovf);
+    o_add(&o->pending_pod_minutes, r->pending_pod_minutes[i], &ovf);
+    o_add(&o->node_min_spot, r->node_min_spot[i], &ovf);
+    o_add(&o->node_min_od, r->node_min_od[i], &ovf);
+    o_add(&o->launches, r->launches[i], &ovf);
+    o_add(&o->deletions, r->deletions[i], &ovf);
+    /* fixed point, as the device totals: microwatt-minutes, micrograms */
+    o_add(&o->energy_uwmin, o_fix(r->energy_wmin[i], 1e6, &ovf), &ovf);
+    o_add(&o->gco2_ug, o_fix(r->gco2[i], 1e6, &ovf), &ovf);
   }
-  o->energy_wmin = (double)o->energy_nwmin * 1e-9;
+  o->energy_wmin = (double)o->energy_uwmin * 1e-6;
   o->gco2 = (double)o->gco2_ug * 1e-6;
+  return ovf ? CCKA_EOVERFLOW : CCKA_OK;
 }

@@ -37,8 +37,9 @@ int ccka_oracle_rollout_policy(const ccka_world* w, const ccka_scenarios* sc, co
                                ccka_results* out, ccka_traj_rec* traj, ccka_detail* detail, const int16_t* act_target,
                                const double* act_cw, uint16_t* feat, int32_t n_threads);
 
-/* Serial totals over results (fixed scenario order). */
-void ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* out);
+/* Serial totals over results (fixed scenario order); CCKA_EOVERFLOW when a
+ * fixed-point sum would leave int64. */
+int ccka_oracle_totals(const ccka_results* r, int64_t n, ccka_totals* out);
 
 /* HPA replica calculator, CPU utilisation target (SEMANTICS §3.C step 3).
  * Returns the proposal; *util_out = utilisation (or -1 if metrics missing). */

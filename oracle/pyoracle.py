@@ -57,6 +57,7 @@ def lib():
                                                  C.POINTER(C.c_int32), C.POINTER(abi.Results),
                                                  C.POINTER(abi.TrajRec), C.c_void_p, C.c_void_p, C.c_void_p,
                                                  C.c_void_p, C.c_int32]
+        L.ccka_oracle_totals.restype = C.c_int
         L.ccka_oracle_totals.argtypes = [C.POINTER(abi.Results), C.c_int64, C.POINTER(abi.Totals)]
         L.ccka_oracle_hpa_resource_proposal.restype = C.c_int32
         L.ccka_oracle_hpa_resource_proposal.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_int32,
@@ -171,7 +172,9 @@ def totals(arrays, n):
     for name, ct, _ in abi.RESULT_FIELDS:
         setattr(r, name, arrays[name].ctypes.data_as(C.POINTER(ct)))
     t = abi.Totals()
-    lib().ccka_oracle_totals(C.byref(r), n, C.byref(t))
+    st = lib().ccka_oracle_totals(C.byref(r), n, C.byref(t))
+    if st != 0:
+        raise OverflowError(f"ccka_oracle_totals: status {st} (a fixed-point total leaves int64)")
     return t
 
 

@@ -2,7 +2,9 @@
 the ctypes mirrors match the C struct layouts, the product path refuses to run
 without a GPU (no CPU fallback), and the multi-rank path (scenario sharding +
 totals all-reduce) reproduces the single-rank totals with world_size 2 over
-gloo."""
+gloo through libccka's own halves of the exchange (ccka_totals_pack /
+ccka_totals_finish); fixed-point totals have headroom and report overflow
+instead of wrapping."""
 import ctypes as C
 import os
 import re
@@ -77,8 +79,16 @@ def _rank_main(rank, world, port, n_per_rank, T, q):
     load = po.gen_load(configs.trace_gen(), T, 1, n, first_id=first)
     res, _ = po.rollout(spec, sc, load, threads=2)
     tot = dist.reduce_totals(po.totals(res, n))
-    if rank == 0:
-        q.put({f: getattr(tot, f) for f in dist.INT_TOTALS + dist.FP_TOTALS})
+    # a rank whose totals could overflow the sum: every rank sees the guard
+    big = po.totals(res, n)
+    if rank == 1:
+        big.energy_uwmin = (1 << 63) - 1 - 10
+    try:
+        dist.reduce_totals(big)
+        ovf = False
+    except OverflowError:
+        ovf = True
+    q.put((rank, ovf, {f: getattr(tot, f) for f in dist.INT_TOTALS + dist.FP_TOTALS}))
     tdist.destroy_process_group()
 
 
@@ -90,7 +100,9 @@ def test_two_rank_gloo_sharding_matches_single_rank():
     procs = [ctx.Process(target=_rank_main, args=(r, 2, port, n_per_rank, T, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    outs = [q.get(timeout=240) for _ in range(2)]
+    got = [o[2] for o in outs if o[0] == 0][0]
+    assert [o[1] for o in outs] == [True, True]  # both ranks refuse the overflowing sum
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -110,3 +122,51 @@ def test_per_scenario_params_are_functions_of_global_id():
     b = configs.hpa_scenarios(400, first_id=600)
     for f in ("target_util_pct", "max_replicas", "cap_sel", "region"):
         assert np.array_equal(getattr(a, f)[600:], getattr(b, f)), f
+
+
+def _synthetic_results(n, energy_wmin, gco2=1.0):
+    from ccka import abi as A
+    arr = {}
+    for name, _, dt in A.RESULT_FIELDS:
+        arr[name] = np.zeros(n, dt)
+    arr["energy_wmin"][:] = energy_wmin
+    arr["gco2"][:] = gco2
+    return arr
+
+
+def test_energy_total_has_headroom_past_the_nanowatt_unit():
+    # 2e6 config-3-sized scenarios (8,590 W.min each, profiles/round3/bench_config3.json):
+    # 1.7e19 nW.min would wrap int64; the microwatt-minute sum is exact
+    n, e = 2_000_000, 8590.125
+    t = po.totals(_synthetic_results(n, e), n)
+    assert t.energy_uwmin == n * 8_590_125_000
+    assert n * int(e * 1e9) > (1 << 63) - 1
+    assert t.energy_wmin == float(n * 8_590_125_000) * 1e-6
+
+
+def test_totals_overflow_is_reported_not_wrapped():
+    with pytest.raises(OverflowError):
+        po.totals(_synthetic_results(1000, 1e13), 1000)  # 1e16 W.min: beyond int64 in uW.min
+    # the host halves of the exchange: a rank's value above INT64_MAX / nranks sets the guard
+    t = abi.Totals()
+    t.energy_uwmin = (1 << 62)
+    blk = dist.pack_totals(t, 1)
+    assert blk[abi.TOTALS_BLOCK - 1] == 0
+    assert dist.finish_totals(blk).energy_uwmin == 1 << 62
+    blk = dist.pack_totals(t, 2)
+    assert blk[abi.TOTALS_BLOCK - 1] == 1
+    with pytest.raises(OverflowError):
+        dist.finish_totals(blk)
+
+
+def test_pack_finish_round_trip_derives_doubles():
+    t = abi.Totals()
+    for k, f in enumerate(dist.INT_TOTALS):
+        setattr(t, f, 1000 * k + 7)
+    blk = dist.pack_totals(t, 8)
+    assert blk[:abi.TOTALS_INT64] == [getattr(t, f) for f in dist.INT_TOTALS]
+    out = dist.finish_totals([8 * v for v in blk])  # as if 8 equal ranks were summed
+    for f in dist.INT_TOTALS:
+        assert getattr(out, f) == 8 * getattr(t, f)
+    assert out.energy_wmin == float(out.energy_uwmin) * 1e-6
+    assert out.gco2 == float(out.gco2_ug) * 1e-6
