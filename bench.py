@@ -66,8 +66,11 @@ def main():
                     help="HPA decision period in seconds (Kubernetes default 15: four decisions per one-minute "
                          "step; 0 = one per step)")
     ap.add_argument("--no-graph", action="store_true",
-                    help="config 5 --mode policy: enqueue the loop's launches directly instead of replaying its "
-                         "captured hipGraph")
+                    help="config 5 --mode policy/grad with --launched: enqueue the loop's launches directly instead "
+                         "of replaying its captured hipGraph")
+    ap.add_argument("--launched", action="store_true",
+                    help="config 5 --mode policy/grad: the launched loop (general kernel + MLP + action kernels per "
+                         "step) instead of the fused one-launch loop")
     ap.add_argument("--spawn", action="store_true",
                     help="run the ranks as fresh child processes even at --gpus 1 (the launcher path)")
     args = ap.parse_args()
@@ -140,6 +143,9 @@ def main():
         fn = eng.lib.ccka_debug_policy_graph
         fn.argtypes = [C.c_void_p, C.c_int32]
         eng._chk(fn(eng.ctx, 0 if args.no_graph else 1), "ccka_debug_policy_graph")
+        fu = eng.lib.ccka_debug_policy_fused
+        fu.argtypes = [C.c_void_p, C.c_int32]
+        eng._chk(fu(eng.ctx, 0 if args.launched else 1), "ccka_debug_policy_fused")
 
         grad_obj = []
 
@@ -256,11 +262,14 @@ def main():
                              "(8 action bins, softmax sampling), objective cost + 0.05 $/kg gCO2 + 0.01 $/SLO-min, "
                              f"score-function gradient over {N * T} (step, cluster) rows"),
                        "clusters_per_gpu": N, "steps": T, "parallelism": f"data-parallel x{world}",
-                       "launch": "direct" if args.no_graph else "hipGraph (captured loop, replayed)"},
+                       "launch": ("fused: one launch per loop (features, MLP on MFMA and actions inside the "
+                                  "rollout's step loop, rollout_kernel<1,8,POL>)") if not args.launched else
+                                 ("launched: direct" if args.no_graph else "launched: hipGraph (captured loop, replayed)")},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
-                         "kernel": "whole loop (mlp_kernel + policy_act_kernel + rollout_kernel per step)" if not grad
-                         else "whole step (closed loop + pg_rows_kernel + pg_wgrad_kernel)",
+                         "kernel": (("whole loop: rollout_kernel<1,8,1> (fused)" if not args.launched else
+                                     "whole loop (mlp_kernel + policy_act_kernel + rollout_kernel per step)")
+                                    if not grad else "whole step (closed loop + pg_rows_kernel + pg_wgrad_kernel)"),
                          "loop_ms_avg": avg_ms, "flops_per_loop": flops},
         }
         if grad:

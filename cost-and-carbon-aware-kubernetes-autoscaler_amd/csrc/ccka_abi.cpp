@@ -139,6 +139,7 @@ struct ccka_ctx {
   hipGraphExec_t pol_graph = nullptr;
   std::vector<unsigned char> pol_graph_key;
   bool pol_graph_off = false;  // ccka_debug_policy_graph(0): launch the sequence directly
+  bool pol_fused_off = false;  // ccka_debug_policy_fused(0): the launched loop even where the fused one applies
   uint16_t* d_feat_rec = nullptr;
   int64_t pol_feat_count = 0;
   // differentiable control (ccka_policy_grad / ccka_mlp_backward, pg.hip)
@@ -1171,6 +1172,56 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
     }
   }
   if ((rc = mlp_alloc(c, N)) != CCKA_OK) return rc;
+  if (pg) {
+    if (!c->d_pg_seed && hipMalloc((void**)&c->d_pg_seed, sizeof(uint64_t)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "seed alloc");
+    // the seed is data, not part of a captured sequence: a new seed replays the graph
+    c->pg_seed_host = pg->seed;
+    HIPCHK(c, hipMemcpyAsync(c->d_pg_seed, &c->pg_seed_host, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+  }
+  // ---- the fused loop (rollout_kernel<1, 8, POL>): one deployment, <= 8 node
+  // slots and the MLP's W2 fragments + biases beside the kernel's LDS ----
+  {
+    const size_t mlp_lds = (size_t)((MLP_HID / 32) * (MLP_HID / 16) + MLP_HID / 16) * 64 * 16 + (2 * MLP_HID + 32) * 4;
+    const size_t off = (lds + 15) & ~(size_t)15;
+    if (!c->pol_fused_off && dmax == 1 && nmax == 8 && off + mlp_lds <= 160 * 1024) {
+      k.t0 = 0;
+      k.t1 = T;
+      k.state = nullptr;
+      k.state_load = 0;
+      k.feat = c->d_mx;  // the last step's features become the MLP states
+      k.w1f = c->d_w1f;
+      k.w2f = c->d_w2f;
+      k.w3f = c->d_w3f;
+      k.mlp_b = c->d_mb;
+      k.pol_seed = pg ? c->d_pg_seed : nullptr;
+      k.rec_target = record ? c->d_rec_target : nullptr;
+      k.rec_cw = record ? c->d_rec_cw : nullptr;
+      k.pol_act = pg ? c->d_pg_act : nullptr;
+      k.feat_rec = feat_on ? c->d_feat_rec : nullptr;
+      k.lds_off_mlp = (int32_t)off;
+      HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+      HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
+      const hipError_t le = launch_rollout_policy(k, off + mlp_lds, pg ? 2 : 1, c->stream);
+      k.feat = nullptr;
+      k.w1f = k.w2f = k.w3f = nullptr;
+      k.mlp_b = nullptr;
+      k.pol_seed = nullptr;
+      k.rec_target = nullptr;
+      k.rec_cw = nullptr;
+      k.pol_act = nullptr;
+      k.feat_rec = nullptr;
+      HIPCHK(c, le);
+      HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+      c->last_engine = 4;
+      c->traj_nt = false;
+      c->traj_valid = trajectory != 0;
+      c->detail_valid = c->detail_on;
+      c->pol_rec_valid = record != 0;
+      c->ran = true;
+      return ccka_sync(c);
+    }
+  }
   MlpParams mp{};
   mp.x = c->d_mx;
   mp.y = c->d_my;
@@ -1200,12 +1251,7 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
     q0.cw = c->d_pol_cw;
     q0.n = N;
     q0.first_id = c->first_id;
-    if (!c->d_pg_seed && hipMalloc((void**)&c->d_pg_seed, sizeof(uint64_t)) != hipSuccess)
-      return fail(c, CCKA_ENOMEM, "seed alloc");
     q0.seed = c->d_pg_seed;
-    // the seed is data, not part of the captured sequence: a new seed replays the graph
-    c->pg_seed_host = pg->seed;
-    HIPCHK(c, hipMemcpyAsync(c->d_pg_seed, &c->pg_seed_host, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
   }
   // the whole loop: state initialisation (t = 0, features of step 0), then
   // per step MLP -> actions -> one rollout step (+ the features kept)
@@ -2081,6 +2127,12 @@ int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
 // Internal: scenarios per wave of the single-deployment kernel (1..64; 0 = automatic).
 // Internal: 0 = enqueue the closed loop's launches directly instead of
 // replaying its captured hipGraph (1, the default)
+int ccka_debug_policy_fused(ccka_ctx* c, int32_t on) {
+  if (!c) return CCKA_EINVAL;
+  c->pol_fused_off = on == 0;
+  return CCKA_OK;
+}
+
 int ccka_debug_policy_graph(ccka_ctx* c, int32_t on) {
   if (!c) return CCKA_EINVAL;
   c->pol_graph_off = on == 0;

@@ -23,6 +23,9 @@ __host__ __device__ constexpr int64_t state_words(int dmax, int nmax) {
   return (int64_t)dmax * (5 + 2 * CCKA_HIST) + 5 * CCKA_MAX_POOLS + (int64_t)nmax * (6 + dmax) + 36;
 }
 
+constexpr int MLP_IN = 64, MLP_HID = 256, MLP_OUT = 8;
+typedef short mlp_bf16x8 __attribute__((ext_vector_type(8)));
+
 struct KParams {
   const ccka_world* w;  // device copy (pools, deployments, scalars)
   const ccka_itype* types;
@@ -74,6 +77,20 @@ struct KParams {
   int32_t lds_off_cap1, lds_off_tile, lds_off_claims, lds_off_misc, lds_off_ci;
   int32_t ablate;  // profiling-only phase switches (0 in every real run)
   int32_t prov[CCKA_MAX_DEPLOY];
+  // fused closed loop (rollout_kernel<1, 8, POL>): the MLP runs inside the step
+  // loop (SEMANTICS 5); POL 1 = deterministic actions, 2 = sampled (the
+  // differentiable-control loop). W2 fragments and the biases in LDS at
+  // lds_off_mlp; W1 / W3 fragments from L2.
+  const mlp_bf16x8* w1f;
+  const mlp_bf16x8* w2f;
+  const mlp_bf16x8* w3f;
+  const float* mlp_b;        // b1 | b2 | b3 (zero-padded to 32)
+  const uint64_t* pol_seed;  // POL 2: the Philox key (device word)
+  int16_t* rec_target;       // [T][N] nullable: the actions of every step
+  double* rec_cw;
+  uint8_t* pol_act;          // POL 2: sampled action bins [T][N]
+  uint16_t* feat_rec;        // nullable: features of steps 0..T [T+1][N][64]
+  int32_t lds_off_mlp, _ppad;
 };
 
 struct GenParams {
@@ -115,6 +132,7 @@ inline void kernel_dims(int D, int maxn, int* dmax, int* nmax) {
 hipError_t launch_gen_load(const GenParams& g, hipStream_t s);
 hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s);
 hipError_t launch_totals(const TotParams& q, int nparts, hipStream_t s);
+hipError_t launch_rollout_policy(const KParams& p, size_t lds, int pol, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Single-deployment HPA engine (rollout_d1.hip): every BASELINE config 2-4
@@ -262,8 +280,6 @@ hipError_t launch_pareto_union(const ccka_grid_stats* gathered, const int64_t* c
 // ---------------------------------------------------------------------------
 // Learned MLP policy (config 5, mlp.hip)
 // ---------------------------------------------------------------------------
-constexpr int MLP_IN = 64, MLP_HID = 256, MLP_OUT = 8;
-typedef short mlp_bf16x8 __attribute__((ext_vector_type(8)));
 struct MlpParams {
   const uint16_t* x;          // [N][64] bf16
   float* y;                   // [N][8]

@@ -433,8 +433,118 @@ __device__ int behavior_long(const ccka_hpa_rules* up, const ccka_hpa_rules* dn,
   return rc < lo ? lo : (rc > hi ? hi : rc);
 }
 
-template <int DMAX, int MAXN>
-__global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout_kernel(KParams p) {
+// ---- the learned policy inside the step loop (fused closed loop, POL > 0) ----
+// The MLP of mlp.hip (H1^T = W1^T X^T, H2^T = W2^T H1^T, Y^T = W3^T H2^T on
+// v_mfma_f32_32x32x16_bf16, each accumulator chained as the next layer's B
+// operand) evaluated on one 32-state tile, with the MFMAs issued in exactly
+// mlp_kernel's accumulation order, so the outputs are bit-identical to the
+// standalone kernel's. W2 fragments and the biases from LDS, W1 / W3 fragments
+// from L2.
+namespace {
+typedef mlp_bf16x8 pbf16x8;
+typedef float pf32x16 __attribute__((ext_vector_type(16)));
+typedef float pf32x4 __attribute__((ext_vector_type(4)));
+typedef short pshort2v __attribute__((ext_vector_type(2)));
+typedef float pf32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pbf16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pf32x16 pmfma(const pbf16x8& a, const pbf16x8& b, const pf32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ pbf16x8 prelu_pack(const pf32x16& a, int s) {
+  pbf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const pbf16x2v b = __builtin_convertvector((pf32x2){a[8 * s + j], a[8 * s + j + 1]}, pbf16x2v);
+    const pshort2v v = __builtin_elementwise_max(__builtin_bit_cast(pshort2v, b), (pshort2v){0, 0});
+    r[j] = v.x;
+    r[j + 1] = v.y;
+  }
+  return r;
+}
+__device__ __forceinline__ pf32x16 pbias_tile(const float* b, int h) {
+  pf32x16 a;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const pf32x4 v = *reinterpret_cast<const pf32x4*>(b + 8 * g + 4 * h);
+    a[4 * g + 0] = v[0];
+    a[4 * g + 1] = v[1];
+    a[4 * g + 2] = v[2];
+    a[4 * g + 3] = v[3];
+  }
+  return a;
+}
+// Y^T of one 32-state tile (xf: its X^T fragments); registers 0..3 of the
+// result = outputs 4h..4h+3 of the lane's column state. W1 fragments come
+// from L2 one row block ahead (their latency hides under the block's MFMAs
+// and epilogue), W2 / W3 fragments and the biases from LDS.
+__device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], const pbf16x8* __restrict__ w1f,
+                                            const pbf16x8* s_w2, const pbf16x8* s_w3, const float* s_b, int lane,
+                                            int h) {
+  constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
+  pbf16x8 hh[KS2];
+  pbf16x8 wc[KS1], wn[KS1];
+#pragma unroll
+  for (int s = 0; s < KS1; ++s) wc[s] = w1f[s * 64 + lane];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    if (n + 1 < NB) {
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) wn[s] = w1f[((n + 1) * KS1 + s) * 64 + lane];
+    }
+    pf32x16 c = pbias_tile(s_b + 32 * n, h);
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) c = pmfma(wc[s], xf[s], c);
+    hh[2 * n] = prelu_pack(c, 0);
+    hh[2 * n + 1] = prelu_pack(c, 1);
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) wc[s] = wn[s];
+    __builtin_amdgcn_sched_barrier(0);  // bounded live ranges: the rollout state shares the register file
+  }
+  pf32x16 y = pbias_tile(s_b + 2 * MLP_HID, h);
+#pragma unroll
+  for (int m = 0; m < NB; ++m) {
+    pf32x16 c = pbias_tile(s_b + MLP_HID + 32 * m, h);
+#pragma unroll
+    for (int kk = 0; kk < KS2; ++kk) c = pmfma(s_w2[(m * KS2 + kk) * 64 + lane], hh[kk], c);
+    y = pmfma(s_w3[(2 * m) * 64 + lane], prelu_pack(c, 0), y);
+    y = pmfma(s_w3[(2 * m + 1) * 64 + lane], prelu_pack(c, 1), y);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return y;
+}
+// v_permlane32_swap_b32: x's lanes 32..63 <-> y's lanes 0..31
+// (tools/probe/permlane.hip documents the lanes). Only for operands held in
+// separate scalars: ROCm 7.2 lowers a swap of two elements of one MFMA
+// accumulator vector with both operands in the same register, so the outputs
+// cross the lane halves by __shfl_xor instead.
+__device__ __forceinline__ void pswap32(uint32_t& x, uint32_t& y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+__device__ __forceinline__ void pol_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                           uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+  for (int q = 0; q < 10; ++q) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+}  // namespace
+
+// POL: 0 = rule-based rollout (steps [t0, t1), resumable); 1 / 2 = the fused
+// closed loop over the whole horizon: before every step the scenario's
+// features, the MLP (MFMA, both 32-lane halves of the wave as two tiles) and
+// the action (1: policy_act_kernel's mapping, 2: policy_sample_kernel's
+// sampling) -- one launch instead of 4T + 1, the state never leaves registers.
+template <int DMAX, int MAXN, int POL = 0>
+__global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout_kernel(KParams p) {
+  static_assert(POL == 0 || (DMAX == 1 && MAXN <= 8), "fused closed loop: one deployment, <= 8 slots");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // world through the constant address space for rare (profile-switch) reads;
   // hot fields are hoisted into registers below
@@ -501,6 +611,20 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
     __syncthreads();
   }
 
+  // fused closed loop: W2 (128 KiB) and W3 (16 KiB) fragments and the biases in LDS
+  constexpr int NW2 = (MLP_HID / 32) * (MLP_HID / 16) * 64, NW3 = (MLP_HID / 16) * 64;
+  const pbf16x8* s_w2 = reinterpret_cast<const pbf16x8*>(smem + p.lds_off_mlp);
+  const pbf16x8* s_w3 = s_w2 + NW2;
+  const float* s_mb = reinterpret_cast<const float*>(s_w3 + NW3);
+  if constexpr (POL != 0) {
+    pbf16x8* dw = reinterpret_cast<pbf16x8*>(smem + p.lds_off_mlp);
+    for (int x = tid; x < NW2; x += blockDim.x) dw[x] = p.w2f[x];
+    for (int x = tid; x < NW3; x += blockDim.x) dw[NW2 + x] = p.w3f[x];
+    float* db = const_cast<float*>(s_mb);
+    for (int x = tid; x < 2 * MLP_HID + 32; x += blockDim.x) db[x] = p.mlp_b[x];
+    __syncthreads();
+  }
+
   // ---- hoisted world fields ----
   Dep dep[DMAX];
 #pragma unroll
@@ -520,7 +644,7 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
 
   // ---- per-scenario parameters ----
   const double cw = active && p.cw ? p.cw[i] : gw->carbon_weight;
-  const double wc1000 = cw * 1000.0;
+  double wc1000 = cw * 1000.0;  // the fused closed loop sets it every step
   const int reset_ca = active && p.reset_ca ? (int)p.reset_ca[i] : gw->reset_ca_s;
   const int pswitch = active && p.pswitch ? (int)p.pswitch[i] : gw->peak_switch;
 
@@ -723,7 +847,137 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
   for (int d = 0; d < DMAX; ++d) Lnext[d] = lptr[((int64_t)min(t0, p.T - 1) * D + (d < D ? d : 0)) * lstride];
   int minute = (gw->start_minute + t0) % 1440;
 
+  // policy features of step tq from the state after step tq - 1 (SEMANTICS 5):
+  // integers scaled by powers of two (exact in fp32), rounded to bf16 -- the
+  // oracle computes the same bits; packed in pairs (feature 2k in the low half
+  // of word k, the memory order of a [64] bf16 row)
+  auto feat_words = [&](int tq, uint32_t (&fw)[32]) {
+    int reps = 0, rd = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      if (d < D) { reps += replicas[d]; rd += rpods[d]; }
+    const int tf = min(tq, p.T - 1);
+    const int mf = (gw->start_minute + tq) % 1440, hf = mf / 60;
+    const bool pk = pswitch && (ps <= pe ? (mf >= ps && mf < pe) : (mf >= ps || mf < pe));
+    uint16_t f[64];
+    f[0] = f2bf(1.0f);
+    f[1] = f2bf((float)reps * 0.0625f);
+    f[2] = f2bf((float)rd * 0.0625f);
+    f[3] = f2bf((float)(reps - rd) * 0.0625f);
+    f[4] = f2bf((float)lptr[((int64_t)tf * D) * lstride] * (1.0f / 1024.0f));
+    f[5] = f2bf((float)nsp);
+    f[6] = f2bf((float)nod);
+    f[7] = f2bf(pk ? 1.0f : 0.0f);
+    f[8] = f2bf((float)s_ci[(rl * 24 + hf) * 2 + 1]);
+    f[9] = f2bf((float)burn * (1.0f / 65536.0f));
+#pragma unroll
+    for (int hh = 0; hh < 24; ++hh) f[10 + hh] = hh == hf ? (uint16_t)0x3F80 : (uint16_t)0;  // bf16 1.0 / 0
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      int pods = 0, code = 0;
+      if (n < MAXN && (used >> n & 1u)) {
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n < MAXN ? n : 0][d] : 0;
+        code = 1 + ni_cap(ninfo[n < MAXN ? n : 0]) + ((rdy >> n & 1u) ? 0 : 2);
+      }
+      f[34 + n] = f2bf((float)pods * 0.0625f);
+      if (n < 14) f[50 + n] = f2bf((float)code);
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) fw[k] = (uint32_t)f[2 * k] | (uint32_t)f[2 * k + 1] << 16;
+  };
+  auto store_feat = [&](uint16_t* row, const uint32_t (&fw)[32]) {
+    uint4* dst = reinterpret_cast<uint4*>(row);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dst[q] = make_uint4(fw[4 * q], fw[4 * q + 1], fw[4 * q + 2], fw[4 * q + 3]);
+  };
+
   for (int t = t0; t < t1; ++t, minute = minute == 1439 ? 0 : minute + 1) {
+    if constexpr (POL != 0) {
+      // ---- the learned policy chooses step t's HPA target and carbon weight ----
+      uint32_t fw[32];
+      feat_words(t, fw);
+      if (p.feat_rec && active) store_feat(p.feat_rec + ((int64_t)t * p.N + i) * 64, fw);
+      // X^T operands of the wave's two 32-state tiles (tile a: the states of
+      // lanes 0..31, tile b: lanes 32..63; lane (r, h) holds features
+      // 16s + 8h .. +7 of state r of the tile): one lane-half swap per word pair
+      pbf16x8 xa[MLP_IN / 16], xb[MLP_IN / 16];
+#pragma unroll
+      for (int s = 0; s < MLP_IN / 16; ++s) {
+        uint32_t wa[4], wb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          wa[j] = fw[8 * s + j];
+          wb[j] = fw[8 * s + 4 + j];
+          pswap32(wa[j], wb[j]);
+        }
+        xa[s] = __builtin_bit_cast(pbf16x8, make_uint4(wa[0], wa[1], wa[2], wa[3]));
+        xb[s] = __builtin_bit_cast(pbf16x8, make_uint4(wb[0], wb[1], wb[2], wb[3]));
+      }
+      const int hl = lane >> 5;
+      pf32x16 ya, yb;
+      if (p.ablate & 32) {  // profiling only: the loop without its MLP
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ya[k] = yb[k] = 0.f;
+      } else {
+        ya = mlp_tile(xa, p.w1f, s_w2, s_w3, s_mb, lane, hl);
+        yb = mlp_tile(xb, p.w1f, s_w2, s_w3, s_mb, lane, hl);
+      }
+      // this lane's state's 8 outputs
+      float y[MLP_OUT] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < (POL == 1 ? 2 : 4); ++k) {  // the deterministic mapping reads y0, y1 only
+        // lanes < 32 own state l of tile a: outputs k (own), 4 + k (lane l + 32);
+        // lanes >= 32 own state l of tile b: outputs k (lane l - 32), 4 + k (own)
+        const float oa = __shfl_xor(ya[k], 32), ob = __shfl_xor(yb[k], 32);
+        y[k] = hl ? ob : ya[k];
+        y[4 + k] = hl ? yb[k] : oa;
+      }
+      int tg;
+      double c;
+      if constexpr (POL == 1) {  // policy_act_kernel
+        const float q0 = rintf(y[0] * 16.0f), q1 = rintf(y[1] * 16.0f);
+        tg = 60 + (int)fminf(fmaxf(q0, -40.0f), 35.0f);
+        c = (double)(int)fminf(fmaxf(q1, 0.0f), 64.0f) / 16.0;
+      } else {  // policy_sample_kernel
+        float pr[MLP_OUT];
+        float mx = y[0];
+#pragma unroll
+        for (int a = 1; a < MLP_OUT; ++a) mx = fmaxf(mx, y[a]);
+        float sum = 0.f;
+#pragma unroll
+        for (int a = 0; a < MLP_OUT; ++a) {
+          pr[a] = expf(y[a] - mx);
+          sum += pr[a];
+        }
+        const int64_t g = p.first_id + i;
+        const uint64_t seed = *p.pol_seed;
+        uint32_t u4[4];
+        pol_philox((uint32_t)g, (uint32_t)(g >> 32), (uint32_t)t, 0x5A3B1E7u, (uint32_t)seed, (uint32_t)(seed >> 32), u4);
+        const float u = (float)(u4[0] >> 8) * (1.0f / 16777216.0f) * sum;
+        int act = MLP_OUT - 1;
+        float acc = 0.f;
+        bool found = false;
+#pragma unroll
+        for (int a = 0; a < MLP_OUT; ++a) {
+          acc += pr[a];
+          if (!found && u < acc) { act = a; found = true; }
+        }
+        tg = 40 + 10 * (act & 3);
+        c = (double)(act >> 2);
+        if (active) p.pol_act[(int64_t)t * p.N + i] = (uint8_t)act;
+      }
+      if (active) {
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          if (d < D && dep[d].scaler == CCKA_SCALER_HPA) target[d] = tg;
+        wc1000 = c * 1000.0;
+        if (p.rec_target) {
+          p.rec_target[(int64_t)t * p.N + i] = (int16_t)tg;
+          p.rec_cw[(int64_t)t * p.N + i] = c;
+        }
+      }
+    }
     int Lcur[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
@@ -2018,43 +2272,11 @@ __global__ void __launch_bounds__(256, (DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout
   }
   if (!active) return;
   if (p.state) state_io(true);
-  if (p.feat) {
-    // policy features of step t1 (SEMANTICS 5): integers scaled by powers of
-    // two (exact in fp32), rounded to bf16 -- the oracle computes the same bits
-    uint16_t* f = p.feat + i * 64;
-    int reps = 0, rd = 0;
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d)
-      if (d < D) { reps += replicas[d]; rd += rpods[d]; }
-    const int tf = min(t1, p.T - 1);
-    const int mf = (gw->start_minute + t1) % 1440, hf = mf / 60;
-    const bool pk = pswitch && (ps <= pe ? (mf >= ps && mf < pe) : (mf >= ps || mf < pe));
-    float v[34];
-    v[0] = 1.0f;
-    v[1] = (float)reps * 0.0625f;
-    v[2] = (float)rd * 0.0625f;
-    v[3] = (float)(reps - rd) * 0.0625f;
-    v[4] = (float)lptr[((int64_t)tf * D) * lstride] * (1.0f / 1024.0f);
-    v[5] = (float)nsp;
-    v[6] = (float)nod;
-    v[7] = pk ? 1.0f : 0.0f;
-    v[8] = (float)s_ci[(rl * 24 + hf) * 2 + 1];
-    v[9] = (float)burn * (1.0f / 65536.0f);
-#pragma unroll
-    for (int h = 0; h < 24; ++h) v[10 + h] = h == hf ? 1.0f : 0.0f;
-#pragma unroll
-    for (int j = 0; j < 34; ++j) f[j] = f2bf(v[j]);
-#pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      int pods = 0, code = 0;
-      if (n < MAXN && (used >> n & 1u)) {
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d) pods += d < D ? npods[n < MAXN ? n : 0][d] : 0;
-        code = 1 + ni_cap(ninfo[n < MAXN ? n : 0]) + ((rdy >> n & 1u) ? 0 : 2);
-      }
-      f[34 + n] = f2bf((float)pods * 0.0625f);
-      if (n < 14) f[50 + n] = f2bf((float)code);
-    }
+  if (p.feat || p.feat_rec) {  // policy features of step t1 (SEMANTICS 5)
+    uint32_t fw[32];
+    feat_words(t1, fw);
+    if (p.feat) store_feat(p.feat + i * 64, fw);
+    if (POL != 0 && p.feat_rec) store_feat(p.feat_rec + ((int64_t)t1 * p.N + i) * 64, fw);
   }
   if (t1 == p.T) gco2 += (double)e_hour * (ci_gpwmin * 1e-9);  // the last hour's carbon (run outputs only)
   if (det && t1 == p.T) {
@@ -2185,6 +2407,10 @@ hipError_t launch_gen_load(const GenParams& g, hipStream_t s) {
 
 hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s) {
   const unsigned grid = (unsigned)((p.N + block - 1) / block);
+#ifdef CCKA_DEV_POL_ONLY  // development builds of the fused loop alone (compile time)
+  (void)grid; (void)lds; (void)s;
+  return hipErrorInvalidValue;
+#else
   if (p.D == 1 && p.maxn <= 8)
     hipLaunchKernelGGL((rollout_kernel<1, 8>), dim3(grid), dim3(block), lds, s, p);
   else if (p.D == 1)
@@ -2193,6 +2419,17 @@ hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s
     hipLaunchKernelGGL((rollout_kernel<4, 16>), dim3(grid), dim3(block), lds, s, p);
   else
     hipLaunchKernelGGL((rollout_kernel<16, 16>), dim3(grid), dim3(block), lds, s, p);
+  return hipGetLastError();
+#endif
+}
+
+// the fused closed loop: the whole horizon in one launch, one 256-thread block
+// (4 waves, one per SIMD) per 256 scenarios
+hipError_t launch_rollout_policy(const KParams& p, size_t lds, int pol, hipStream_t s) {
+  const unsigned grid = (unsigned)((p.N + 255) / 256);
+  if (p.D != 1 || p.maxn > 8 || (pol != 1 && pol != 2)) return hipErrorInvalidValue;
+  if (pol == 1) hipLaunchKernelGGL((rollout_kernel<1, 8, 1>), dim3(grid), dim3(256), lds, s, p);
+  else hipLaunchKernelGGL((rollout_kernel<1, 8, 2>), dim3(grid), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ def test_closed_loop_policy_parity(engine, drift):
         fg = engine.debug_get_policy_features()
     finally:
         engine.debug_policy_features(False)
-    assert engine.last_engine()[0] == 3
+    assert engine.last_engine()[0] == 4  # the fused loop (one launch, MLP inside the step loop)
     assert at.std() > 0 and len(np.unique(at)) >= 3  # the policy really steers
     # 1. the rollout under the recorded actions and every step's features: bit-exact
     rc, tc, fc = po.rollout_policy(spec, sc, load, at, ac, traj=True, threads=THREADS, features=True)
@@ -91,13 +91,16 @@ def test_closed_loop_policy_parity(engine, drift):
 
 
 @pytest.mark.gpu
-def test_closed_loop_graph_replay_identical(engine):
-    """The closed loop runs as one captured hipGraph (replayed while its inputs
-    are unchanged): a first call (capture), a second (replay) and a direct
-    launch sequence give bit-identical results, trajectories and actions; new
-    scenarios force a fresh capture."""
+@pytest.mark.parametrize("drift", [0, 1])
+def test_closed_loop_fused_equals_launched(engine, drift):
+    """The fused loop (rollout_kernel<1, 8, 1>: features, MLP and actions inside
+    the step loop, one launch) against the launched loop (resumable general
+    kernel + mlp_kernel + policy_act_kernel per step, as a captured hipGraph:
+    first call = capture, second = replay, then direct launches): results,
+    trajectories, actions, every step's features and the final MLP states are
+    bit-identical; new scenarios force a fresh capture."""
     import ctypes as C
-    spec, sc, load = _case(drift=0)
+    spec, sc, load = _case(drift=drift)
     ws, bs = configs.mlp_weights(11)
     engine.set_world(spec)
     engine.set_scenarios(sc)
@@ -105,15 +108,37 @@ def test_closed_loop_graph_replay_identical(engine):
     engine.mlp_set_weights([configs.to_bf16_bits(w) for w in ws], bs)
     fn = engine.lib.ccka_debug_policy_graph
     fn.argtypes = [C.c_void_p, C.c_int32]
+    fu = engine.lib.ccka_debug_policy_fused
+    fu.argtypes = [C.c_void_p, C.c_int32]
     runs = []
-    for graph in (1, 1, 0):
-        fn(engine.ctx, graph)
-        engine.policy_rollout(trajectory=True, record=True)
-        runs.append((engine.results(), engine.trajectory(), engine.policy_actions()))
-    fn(engine.ctx, 1)
-    for r, t, (at, ac) in runs[1:]:
+    engine.debug_policy_features(True)
+    try:
+        for fused, graph in ((1, 1), (0, 1), (0, 1), (0, 0)):
+            fu(engine.ctx, fused)
+            fn(engine.ctx, graph)
+            engine.policy_rollout(trajectory=True, record=True)
+            assert engine.last_engine()[0] == (4 if fused else 3)
+            runs.append((engine.results(), engine.trajectory(), engine.policy_actions(),
+                         engine.debug_get_policy_features()))
+    finally:
+        fu(engine.ctx, 1)
+        fn(engine.ctx, 1)
+        engine.debug_policy_features(False)
+    for r, t, (at, ac), f in runs[1:]:
         compare(r, runs[0][0], t, runs[0][1])
         assert np.array_equal(at, runs[0][2][0]) and np.array_equal(ac, runs[0][2][1])
+        assert np.array_equal(f, runs[0][3])
+    # the MLP states left behind are the last step's features (ccka.h)
+    engine.mlp_n = sc.n
+    engine.mlp_forward()
+    y_last = engine.mlp_actions()
+    fu(engine.ctx, 0)
+    try:
+        engine.policy_rollout(trajectory=False, record=False)
+        engine.mlp_forward()
+        assert np.array_equal(engine.mlp_actions(), y_last)
+    finally:
+        fu(engine.ctx, 1)
     sc2 = configs.hpa_scenarios(sc.n, first_id=777)
     engine.set_scenarios(sc2)
     engine.set_load(load)

@@ -1,4 +1,4 @@
-// permlane.hip — semantics of __builtin_amdgcn_permlane32_swap on gfx950
+// permlane.hip — semantics of v_permlane32_swap_b32 (__builtin_amdgcn_permlane32_swap) on gfx950
 // (diagnostic): lane l passes (X = 100 + l, Y = 200 + l); prints what lanes 0,
 // 1, 32, 33 get back in each element. Build: hipcc -O3 --offload-arch=gfx950
 #include <hip/hip_runtime.h>
