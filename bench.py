@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--launched", action="store_true",
                     help="config 5 --mode policy/grad: the launched loop (general kernel + MLP + action kernels per "
                          "step) instead of the fused one-launch loop")
+    ap.add_argument("--trace-flat", action="store_true",
+                    help="single-deployment kernel: read the [T][N] load trace instead of its wave-tiled copy "
+                         "(layout A/B; same results)")
     ap.add_argument("--spawn", action="store_true",
                     help="run the ranks as fresh child processes even at --gpus 1 (the launcher path)")
     args = ap.parse_args()
@@ -192,6 +195,10 @@ def main():
                 pool.budget_pct = args.budget
         eng.set_world(spec)
         eng.set_scenarios(sc)
+        if args.trace_flat:
+            tf = eng.lib.ccka_debug_trace_flat
+            tf.argtypes = [C.c_void_p, C.c_int32]
+            eng._chk(tf(eng.ctx, 1), "ccka_debug_trace_flat")
         eng.gen_load(gen)
         if cfg == 4:
             comm_init()
@@ -330,11 +337,12 @@ def main():
                        + (f", disruption budget {args.budget} %" if args.budget is not None else ""),
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
+                       "trace_layout": "[T][N] (shared traces)" if cfg == 4 else "[T][N]" if args.trace_flat else "wave-tiled [wave][T][lanes] (built at gen_load)",
                        "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None if args.drift or args.replace or args.multi or args.hpa_sync not in (0, 60)
-                         or args.budget is not None
+                         or args.budget is not None or args.trace_flat
                          else measured_traffic(cfg, traj, N, T),
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,

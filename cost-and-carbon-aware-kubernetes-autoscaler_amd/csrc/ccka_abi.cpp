@@ -56,6 +56,11 @@ struct ccka_ctx {
   int32_t* d_load = nullptr;
   int64_t load_count = 0;
   bool have_load = false;
+  // wave-tiled copy of the trace for the single-deployment kernel (d1_trace_tile)
+  int32_t* d_load_w = nullptr;
+  int64_t load_w_count = 0;
+  int32_t load_w_lpw = 0;  // lanes per wave it was tiled for (0: stale)
+  bool trace_flat = false;  // ccka_debug_trace_flat: read [T][N] (A/B of the layout)
   void* d_res = nullptr;  // one allocation, SoA carve
   KParams kp{};
   ccka_traj_rec* d_traj = nullptr;
@@ -140,6 +145,11 @@ struct ccka_ctx {
   std::vector<unsigned char> pol_graph_key;
   bool pol_graph_off = false;  // ccka_debug_policy_graph(0): launch the sequence directly
   bool pol_fused_off = false;  // ccka_debug_policy_fused(0): the launched loop even where the fused one applies
+  bool pol_table_off = false;  // ccka_debug_policy_table(0): the fused loop's catalog scans instead of the tables
+  int2* d_ptable = nullptr;    // the fused loop's argmin tables (65 policy carbon weights)
+  int32_t* d_pjtab = nullptr;
+  double* d_pwc = nullptr;
+  int64_t ptable_count = 0;
   uint16_t* d_feat_rec = nullptr;
   int64_t pol_feat_count = 0;
   // differentiable control (ccka_policy_grad / ccka_mlp_backward, pg.hip)
@@ -153,7 +163,7 @@ struct ccka_ctx {
   int64_t pg_coef_count = 0;
   uint16_t* d_pg_x = nullptr;    // ccka_mlp_backward's rows [M][64]
   int64_t pg_x_count = 0;
-  uint16_t* d_pg_work = nullptr; // xT | h1T | h2T | dh1T | dh2T | gyT | ones, each [rows][Mpad]
+  uint16_t* d_pg_work = nullptr; // xT | h1T | h2T | dh1T | dh2T | gyT, each row-blocked [Mpad/16][units][16]
   int64_t pg_work_count = 0;
   float* d_pg_part = nullptr;    // weight-gradient row-split partials
   int64_t pg_part_count = 0;
@@ -576,7 +586,8 @@ void ccka_close(ccka_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   dfree(c->d_world); dfree(c->d_types); dfree(c->d_price); dfree(c->d_ci_gpwh); dfree(c->d_ci_gpwmin);
   dfree(c->d_region); dfree(c->d_target); dfree(c->d_maxr); dfree(c->d_dstab); dfree(c->d_resetca);
-  dfree(c->d_pswitch); dfree(c->d_cw); dfree(c->d_capsel); dfree(c->d_load); dfree(c->d_totals);
+  dfree(c->d_pswitch); dfree(c->d_cw); dfree(c->d_capsel); dfree(c->d_load); dfree(c->d_load_w); dfree(c->d_totals);
+  dfree(c->d_ptable); dfree(c->d_pjtab); dfree(c->d_pwc);
   dfree(c->d_sinq);
   dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
@@ -770,6 +781,9 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   c->n_traces = sc->n_traces;
   if ((rc = alloc_results(c)) != CCKA_OK) return rc;
   dfree(c->d_load);
+  dfree(c->d_load_w);
+  c->load_w_count = 0;
+  c->load_w_lpw = 0;
   c->have_load = false;
   c->have_sc = true;
   c->ran = false;
@@ -788,6 +802,44 @@ static int ensure_load(ccka_ctx* c) {
   return CCKA_OK;
 }
 
+// scenarios per wave of the single-deployment kernel: a wave's cost is the
+// union of its lanes' event paths, so when the batch is smaller than one full
+// round of resident waves (two per SIMD at this kernel's register budget)
+// spread it over all of them
+static int32_t d1_lpw(const ccka_ctx* c) {
+  if (c->lpw > 0) return c->lpw;
+  const int64_t slots = 2LL * 4 * c->cus;  // resident waves: 2 per SIMD, 4 SIMDs per CU
+  return (int32_t)std::min<int64_t>(64, std::max<int64_t>(32, (c->N + slots - 1) / slots));
+}
+
+// The single-deployment kernel reads a per-scenario trace wave-tiled
+// ([wave][T][lanes]): with [T][N] a wave's 196-byte row shares its first and
+// last 128-byte lines with the neighbouring waves, which run up to hundreds of
+// steps apart (lane skew), so the L2 has evicted those lines before the
+// neighbour reads them. Built once per trace (set_load / gen_load) and lanes-
+// per-wave value, beside the [T][N] trace the other paths read; without the
+// memory for it the kernel reads [T][N] (same results).
+static int d1_trace_tile(ccka_ctx* c) {
+  if (!c->d1_world || c->hw.n_deploy != 1 || c->n_traces > 0 || !c->have_load) return CCKA_OK;
+  const int32_t lpw = d1_lpw(c);
+  if (c->load_w_lpw == lpw && c->d_load_w) return CCKA_OK;
+  const int64_t cnt = (int64_t)c->hw.n_steps * c->N;
+  if (!c->d_load_w || c->load_w_count != cnt) {
+    dfree(c->d_load_w);
+    c->load_w_count = 0;
+    if (hipMalloc((void**)&c->d_load_w, (size_t)cnt * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      c->d_load_w = nullptr;
+      return CCKA_OK;
+    }
+    c->load_w_count = cnt;
+  }
+  HIPCHK(c, launch_trace_tile(c->d_load, c->d_load_w, c->N, c->hw.n_steps, lpw, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->load_w_lpw = lpw;
+  return CCKA_OK;
+}
+
 int ccka_set_load(ccka_ctx* c, const int32_t* load, int64_t count) {
   if (!c || !load) return CCKA_EINVAL;
   if (!c->have_sc) return fail(c, CCKA_ESTATE, "set_scenarios first");
@@ -795,10 +847,11 @@ int ccka_set_load(ccka_ctx* c, const int32_t* load, int64_t count) {
   int rc;
   if ((rc = ensure_load(c)) != CCKA_OK) return rc;
   if (count != c->load_count) return fail(c, CCKA_EINVAL, "load count %lld != T*D*N %lld", (long long)count, (long long)c->load_count);
+  c->load_w_lpw = 0;
   HIPCHK(c, hipMemcpyAsync(c->d_load, load, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_load = true;
-  return CCKA_OK;
+  return d1_trace_tile(c);
 }
 
 int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
@@ -822,10 +875,11 @@ int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
   gp.amp_lo = g->amp_lo_pm; gp.amp_hi = g->amp_hi_pm;
   gp.noise = g->noise_pm; gp.burst_prob = g->burst_prob_pm;
   gp.burst_mult = g->burst_mult_pm; gp.burst_len = g->burst_len;
+  c->load_w_lpw = 0;
   HIPCHK(c, launch_gen_load(gp, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_load = true;
-  return CCKA_OK;
+  return d1_trace_tile(c);
 }
 
 int ccka_get_load(ccka_ctx* c, int32_t* load, int64_t count) {
@@ -1012,14 +1066,11 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     p.first_id = k.first_id;
     p.NW = c->NW;
     p.occ = c->occ > 0 ? c->occ : 2;  // higher targets spill (measured slower: tools/occ.py)
-    // scenarios per wave: a wave's cost is the union of its lanes' event paths,
-    // so when the batch is smaller than one full round of resident waves (two
-    // per SIMD at this kernel's register budget) spread it over all of them
-    if (c->lpw > 0) {
-      p.lpw = c->lpw;
-    } else {
-      const int64_t slots = 2LL * 4 * c->cus;  // resident waves: 2 per SIMD, 4 SIMDs per CU
-      p.lpw = (int32_t)std::min<int64_t>(64, std::max<int64_t>(32, (c->N + slots - 1) / slots));
+    p.lpw = d1_lpw(c);
+    p.load_w = nullptr;
+    if (!c->trace_flat) {
+      if ((rc = d1_trace_tile(c)) != CCKA_OK) return rc;
+      if (c->load_w_lpw == p.lpw && c->d_load_w && p.trace_mod == 0) p.load_w = c->d_load_w;
     }
     p.ablate = k.ablate;
     p.stamps = nullptr;
@@ -1106,6 +1157,54 @@ static int mlp_alloc(ccka_ctx* c, int64_t n);
 // (policy_act_kernel); otherwise each step samples an action bin from
 // softmax(y) (policy_sample_kernel) and the features and actions of every
 // step are kept for the score-function gradient (ccka_policy_grad).
+// The fused loop's Karpenter launches on a single-deployment world without
+// pool limits (d1_check_world) read argmin tables instead of scanning the
+// catalog: table_kernel over every carbon weight the policy can emit (k / 16,
+// k = 0..64; the sampled policy's 0 and 1 are k = 0 and 16), rebuilt per loop
+// on the stream (prices and carbon intensity are the world's). Leaves
+// k->ptable null when the world does not qualify.
+static int policy_tables(ccka_ctx* c, KParams* k) {
+  const ccka_world& w = c->hw;
+  if (!c->d1_world || w.n_zones > 4 || c->zmasks.empty()) return CCKA_OK;
+  constexpr int NWP = 65;
+  const int64_t keys = (int64_t)w.n_regions * 24 * (int64_t)c->zmasks.size() * 3;
+  const int64_t cnt = keys * NWP * c->JT;
+  if (c->ptable_count != cnt) {
+    dfree(c->d_ptable);
+    dfree(c->d_pjtab);
+    c->ptable_count = 0;
+    if (hipMalloc((void**)&c->d_ptable, (size_t)cnt * sizeof(int2)) != hipSuccess ||
+        hipMalloc((void**)&c->d_pjtab, (size_t)keys * sizeof(int32_t)) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "policy argmin table alloc (%lld entries)", (long long)cnt);
+    c->ptable_count = cnt;
+  }
+  if (!c->d_pwc) {
+    double wc[NWP];
+    for (int x = 0; x < NWP; ++x) wc[x] = (double)x / 16.0 * 1000.0;  // the kernel's c * 1000.0
+    int rc;
+    if ((rc = dupload(c, c->d_pwc, wc, (size_t)NWP)) != CCKA_OK) return rc;
+  }
+  TableParams tp{};
+  tp.price = c->d_price; tp.ci_gpwh = c->d_ci_gpwh; tp.types = c->d_types;
+  tp.order = c->d_order; tp.cap1s = c->d_cap1s; tp.zmasks = c->d_zmasks; tp.wc1000 = c->d_pwc;
+  tp.table = c->d_ptable; tp.jtab = c->d_pjtab;
+  tp.K = w.n_types; tp.Z = w.n_zones; tp.R = w.n_regions; tp.NZI = (int)c->zmasks.size();
+  tp.NW = NWP; tp.JT = c->JT;
+  HIPCHK(c, launch_table(tp, c->stream));
+  k->ptable = c->d_ptable;
+  k->pjtab = c->d_pjtab;
+  k->pNZI = tp.NZI;
+  k->pJT = c->JT;
+  k->pNW = NWP;
+  const uint32_t zall = (1u << w.n_zones) - 1u;
+  for (uint32_t m = 0; m < 16; ++m) {
+    k->pzmi[m] = -1;
+    for (size_t z = 0; z < c->zmasks.size(); ++z)
+      if ((m & zall) && c->zmasks[z] == (m & zall)) k->pzmi[m] = (int32_t)z;
+  }
+  return CCKA_OK;
+}
+
 static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const ccka_pg_params* pg) {
   if (!c) return CCKA_EINVAL;
   c->pg_valid = false;  // the recorded features / actions are about to be overwritten
@@ -1201,8 +1300,12 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
       k.feat_rec = feat_on ? c->d_feat_rec : nullptr;
       k.lds_off_mlp = (int32_t)off;
       HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+      k.ptable = nullptr;
+      if (!c->pol_table_off && (rc = policy_tables(c, &k)) != CCKA_OK) return rc;
       HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
       const hipError_t le = launch_rollout_policy(k, off + mlp_lds, pg ? 2 : 1, c->stream);
+      k.ptable = nullptr;
+      k.pjtab = nullptr;
       k.feat = nullptr;
       k.w1f = k.w2f = k.w3f = nullptr;
       k.mlp_b = nullptr;
@@ -1359,7 +1462,7 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
   if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
   if (M < 1 || n_scen < 1) return fail(c, CCKA_EINVAL, "no rows");
   const int64_t Mpad = (M + 31) / 32 * 32;
-  const int64_t rows = 64 + 4 * MLP_HID + 8 + 1;  // xT h1T h2T dh1T dh2T gyT ones
+  const int64_t rows = 64 + 4 * MLP_HID + 8;  // xT h1T h2T dh1T dh2T gyT
   if (c->pg_work_count < rows * Mpad) {
     dfree(c->d_pg_work);
     c->pg_work_count = 0;
@@ -1375,8 +1478,6 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
   uint16_t* dh1T = h2T + MLP_HID * Mpad;
   uint16_t* dh2T = dh1T + MLP_HID * Mpad;
   uint16_t* gyT = dh2T + MLP_HID * Mpad;
-  uint16_t* ones = gyT + 8 * Mpad;
-  HIPCHK(c, launch_pg_fill(ones, Mpad, M, 0x3F80 /* bf16 1.0 */, c->stream));
   PgRowsParams rp{};
   rp.x = x;
   rp.act = act;
@@ -1394,16 +1495,17 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
   HIPCHK(c, launch_pg_rows(rp, c->cus, c->stream));
   // the six reductions over rows; row splits fill the chip, >= 256 rows each,
   // fixed for a given Mpad (deterministic sums)
-  struct G { const uint16_t* a; int ka; const uint16_t* b; int kb; int64_t off; };
+  // the three weight-gradient GEMMs over all rows, each with its bias gradient
+  // (the row sums of its B operand) folded in: dW1 | db1, dW2 | db2, dW3 | db3
+  struct G { const uint16_t* a; int ka; const uint16_t* b; int kb; int64_t off, boff; };
   const int64_t o_b1 = 64 * 256, o_w2 = o_b1 + 256, o_b2 = o_w2 + 256 * 256, o_w3 = o_b2 + 256, o_b3 = o_w3 + 256 * 8;
-  const G gs[6] = {{xT, 64, dh1T, MLP_HID, 0}, {dh1T, MLP_HID, ones, 1, o_b1}, {h1T, MLP_HID, dh2T, MLP_HID, o_w2},
-                   {dh2T, MLP_HID, ones, 1, o_b2}, {h2T, MLP_HID, gyT, MLP_OUT, o_w3}, {gyT, MLP_OUT, ones, 1, o_b3}};
-  auto splits_of = [&](const G& g) {
-    const int64_t tiles = (int64_t)((g.ka + 31) / 32) * ((g.kb + 31) / 32);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(2048 / tiles, Mpad / 256));
-  };
+  const G gs[3] = {{xT, 64, dh1T, MLP_HID, 0, o_b1}, {h1T, MLP_HID, dh2T, MLP_HID, o_w2, o_b2},
+                   {h2T, MLP_HID, gyT, MLP_OUT, o_w3, o_b3}};
+  // one workgroup per CU owns a chunk of rows and the whole output (pg.hip);
+  // the split count is fixed for a given Mpad (deterministic sums)
+  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(c->cus, Mpad / 256));
   int64_t need = 0;
-  for (const G& g : gs) need = std::max<int64_t>(need, (int64_t)splits_of(g) * g.ka * g.kb);
+  for (const G& g : gs) need = std::max<int64_t>(need, (int64_t)splits * (g.ka * g.kb + g.kb));
   if (c->pg_part_count < need) {
     dfree(c->d_pg_part);
     c->pg_part_count = 0;
@@ -1416,11 +1518,12 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
     q.A = g.a;
     q.B = g.b;
     q.part = c->d_pg_part;
+    q.bpart = c->d_pg_part + (int64_t)splits * g.ka * g.kb;
     q.Mpad = Mpad;
     q.KA = g.ka;
     q.KB = g.kb;
-    q.splits = splits_of(g);
-    HIPCHK(c, launch_pg_wgrad(q, c->d_pg_grad + g.off, c->stream));
+    q.splits = splits;
+    HIPCHK(c, launch_pg_wgrad(q, c->d_pg_grad + g.off, c->d_pg_grad + g.boff, c->stream));
   }
   return CCKA_OK;
 }
@@ -1512,11 +1615,11 @@ int ccka_policy_grad(ccka_ctx* c, const ccka_pg_params* pg, ccka_mlp_grads* out,
 }
 
 // Internal (tests): the backward's unit-major work arrays of the last
-// ccka_mlp_backward / ccka_policy_grad: xT | h1T | h2T | dh1T | dh2T | gyT |
-// ones, each [rows][Mpad] bf16; *mpad receives Mpad.
+// ccka_mlp_backward / ccka_policy_grad: xT | h1T | h2T | dh1T | dh2T | gyT,
+// each row-blocked [Mpad/16][units][16] bf16; *mpad receives Mpad.
 int ccka_debug_pg_work(ccka_ctx* c, uint16_t* out, int64_t count, int64_t* mpad) {
   if (!c || !out || !mpad || !c->d_pg_work) return CCKA_EINVAL;
-  const int64_t rows = 64 + 4 * MLP_HID + 8 + 1;
+  const int64_t rows = 64 + 4 * MLP_HID + 8;
   if (count < c->pg_work_count) return fail(c, CCKA_EINVAL, "need %lld", (long long)c->pg_work_count);
   (void)hipSetDevice(c->device);
   *mpad = c->pg_work_count / rows;
@@ -2127,6 +2230,14 @@ int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
 // Internal: scenarios per wave of the single-deployment kernel (1..64; 0 = automatic).
 // Internal: 0 = enqueue the closed loop's launches directly instead of
 // replaying its captured hipGraph (1, the default)
+// Internal: 0 = the fused loop scans the catalog for its launches (A/B of the
+// argmin tables; same results).
+int ccka_debug_policy_table(ccka_ctx* c, int32_t on) {
+  if (!c) return CCKA_EINVAL;
+  c->pol_table_off = on == 0;
+  return CCKA_OK;
+}
+
 int ccka_debug_policy_fused(ccka_ctx* c, int32_t on) {
   if (!c) return CCKA_EINVAL;
   c->pol_fused_off = on == 0;
@@ -2142,6 +2253,14 @@ int ccka_debug_policy_graph(ccka_ctx* c, int32_t on) {
 int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
   if (!c || lpw < 0 || lpw > 64) return CCKA_EINVAL;
   c->lpw = lpw;
+  return CCKA_OK;
+}
+
+// Internal: 1 = the single-deployment kernel reads the [T][N] trace instead of
+// its wave-tiled copy (layout A/B; results are the same).
+int ccka_debug_trace_flat(ccka_ctx* c, int32_t on) {
+  if (!c) return CCKA_EINVAL;
+  c->trace_flat = on != 0;
   return CCKA_OK;
 }
 

@@ -91,6 +91,13 @@ struct KParams {
   uint8_t* pol_act;          // POL 2: sampled action bins [T][N]
   uint16_t* feat_rec;        // nullable: features of steps 0..T [T+1][N][64]
   int32_t lds_off_mlp, _ppad;
+  // fused loop on a single-deployment world without pool limits: provisioning
+  // by the argmin tables of table_kernel over the policy's 65 carbon weights
+  // (k / 16, k = 0..64) instead of the wave-cooperative catalog scans
+  const int2* ptable;        // nullable: [R*24][NZI][3][65][JT]
+  const int32_t* pjtab;      // [R*24][NZI][3] J (largest pod count of an offered type)
+  int32_t pNZI, pJT, pNW, _ppad2;
+  int32_t pzmi[16];          // zone mask -> zone-mask index of the tables (-1: none)
 };
 
 struct GenParams {
@@ -182,6 +189,7 @@ struct D1Patch {
 
 struct D1Params {
   const int32_t* load;       // [T][N]
+  const int32_t* load_w;     // the same trace wave-tiled [wave][T][lanes] (nullptr: read `load`)
   const int32_t* price;      // [R][24][K][Z][2]
   const double* ci_gpwmin;   // [R][24]
   const long long* acc;      // [K][3] idle_nw, dyn_nw_per_m, alloc_cpu_m
@@ -255,6 +263,7 @@ struct TableParams {
 };
 
 hipError_t launch_table(const TableParams& t, hipStream_t s);
+hipError_t launch_trace_tile(const int32_t* in, int32_t* out, int64_t N, int64_t T, int32_t lpw, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Policy sweep (config 4): per-grid sums and the Pareto frontier (sweep.hip)
@@ -326,19 +335,22 @@ struct PgRowsParams {
   const mlp_bf16x8* w2b;    // [8 row blocks][16 k-steps][64]: A fragments of dH1^T = W2 dH2^T
   const mlp_bf16x8* w3b;    // [8][64]: A fragments of dH2^T = W3 g_y^T (k = action, padded to 16)
   const float* bias;        // b1 | b2 | b3 (zero-padded), as MlpParams
-  uint16_t *xT, *h1T, *h2T, *dh1T, *dh2T, *gyT;  // [64|256|256|256|256|8][Mpad]
+  // row-blocked [Mpad/16][64|256|256|256|256|8][16] (element (u, m) at ((m/16) U + u) 16 + m%16)
+  uint16_t *xT, *h1T, *h2T, *dh1T, *dh2T, *gyT;
   int64_t M, Mpad, n_scen;
 };
 hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s);
-// C[KA][KB] = sum_m A[a][m] B[b][m] over unit-major bf16 operands (fp32 result)
+// C[KA][KB] = sum_m A[a][m] B[b][m] over row-blocked bf16 operands (fp32 result)
 struct WgradParams {
-  const uint16_t* A;  // [KA][Mpad]
-  const uint16_t* B;  // [KB][Mpad]
+  const uint16_t* A;  // [Mpad/16][KA][16]
+  const uint16_t* B;  // [Mpad/16][KB][16]
   float* part;        // [splits][KA][KB]
+  float* bpart;       // nullable: [splits][KB] column sums of B (the bias gradient)
   int64_t Mpad;
   int32_t KA, KB, splits, _pad;
 };
-hipError_t launch_pg_wgrad(const WgradParams& q, float* out, hipStream_t s);
+// out = A B^T summed over rows; out_bias (nullable) = the row sums of B
+hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, hipStream_t s);
 hipError_t launch_pg_fill(uint16_t* x, int64_t n, int64_t valid, uint16_t v, hipStream_t s);
 // [N][T] (single-deployment engine, device side) -> steps [t0, t0 + tc) of the
 // [T][N] order ccka_get_trajectory returns, into out[tc][N]

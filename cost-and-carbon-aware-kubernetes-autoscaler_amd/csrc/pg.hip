@@ -15,17 +15,23 @@
 //                    dH2^T = W3 g_y^T (masked by H2 > 0) and dH1^T = W2 dH2^T
 //                    (masked by H1 > 0) with the same in-register operand
 //                    chaining; it stores X^T, H1^T, H2^T, dH1^T, dH2^T, g_y^T
-//                    unit-major ([unit][row], rows padded to 32)
+//                    row-blocked ([row / 16][unit][16]: a unit's 16 rows of a
+//                    block in one 32-byte run), transposed through LDS so each
+//                    store instruction writes whole 512-byte runs
 //   pg_wgrad_kernel  C[a][b] = sum_m A[a][m] B[b][m] over millions of rows:
-//                    one 32x32 output tile per wave, 16 rows per MFMA k-step,
-//                    both operands 16-byte loads from the unit-major arrays;
-//                    row-split partials summed in a fixed order (deterministic)
+//                    one 8-wave workgroup per CU owns a chunk of rows and the
+//                    whole output, 16 rows per MFMA k-step; an operand fragment
+//                    (32 units x 16 rows) is ONE contiguous 1 KB run of the
+//                    row-blocked arrays; row-split partials summed in a fixed
+//                    order (deterministic)
 // dW1 = X^T dH1, dW2 = H1^T dH2, dW3 = H2^T g_y, db = the same with a ones row.
 // Anchor: the controller chooses "the cheapest and cleanest number of pods and
 // node types that still meet the SLO" (CS218_Project_Proposal.pdf p.1) and the
 // dashboards plot cost / carbon / SLO trade-offs (p.5). SEMANTICS 5.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "kparams.h"
 
@@ -104,18 +110,38 @@ __device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
   return a;
 }
 
-// hidden unit of element j of k-step fragment q for lane half h (the
-// accumulator row order the forward chains through, mlp.hip)
-__device__ __forceinline__ int kin(int q, int j, int h) { return 16 * q + 8 * (j >> 2) + 4 * h + (j & 3); }
 
-// one fragment's 8 values of this lane's row into a unit-major [unit][Mpad]
-// array: `col` points at (unit 4h, this row); the unit offsets are wave-uniform
-__device__ __forceinline__ void store_frag(uint16_t* __restrict__ col, int64_t Mpad, int q, const bf16x8& v) {
+// Row-blocked work arrays: element (unit u, row m) of a U-unit array sits at
+// ((m / 16) * U + u) * 16 + m % 16, so the 16 rows of a block are contiguous
+// per unit and a wgrad operand fragment (32 units x 16 rows) is one 1 KB run.
+__device__ __forceinline__ int64_t rb_off(int64_t m, int U, int u) { return ((m >> 4) * U + u) * 16 + (m & 15); }
+
+// One 16-unit fragment of this wave's 32-row tile into a row-blocked array:
+// lane (row r, half h) holds units o(j, h), j = 0..7, of row r; they go to the
+// wave's 1 KB LDS tile as [unit][row], come back as 8 consecutive rows of one
+// unit per lane (16 B), and each store instruction writes two 512-byte runs
+// (units u0..u0+15 of rows 0-15 and of rows 16-31). Only units < U are stored.
+template <class O>
+__device__ __forceinline__ void store_rows(uint16_t* __restrict__ arr, int U, int u0, int64_t tile, const bf16x8& v,
+                                           uint16_t* s_tr, int lane, O o) {
+  const int r = lane & 31, h = lane >> 5;
   const u32x4_ d = __builtin_bit_cast(u32x4_, v);
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    col[(int64_t)(16 * q + 8 * (j >> 2) + (j & 3)) * Mpad] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+  for (int j = 0; j < 8; ++j) s_tr[o(j, h) * 32 + r] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int uu = lane >> 2, rg = lane & 3;
+  const u32x4_ w = *reinterpret_cast<const u32x4_*>(s_tr + uu * 32 + 8 * rg);
+  if (u0 + uu < U) *reinterpret_cast<u32x4_*>(arr + rb_off(tile * 32 + 8 * rg, U, u0 + uu)) = w;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// hidden-unit fragment q (the accumulator row order, kin) / input fragment s
+// (units 16 s + 8 h + j) / action fragment (h = 0: actions 0..7)
+__device__ __forceinline__ int o_kin(int j, int h) { return 8 * (j >> 2) + 4 * h + (j & 3); }
+__device__ __forceinline__ int o_lin(int j, int h) { return 8 * h + j; }
 
 __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
                                        uint32_t out[4]) {
@@ -182,7 +208,9 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
   constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
   __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 32];
   __shared__ bf16x8 s_w2[NB * KS2 * WAVE];  // forward W2 fragments, 128 KiB
+  __shared__ __attribute__((aligned(16))) uint16_t s_trans[4][16 * 32];  // per wave: a fragment's [unit][row]
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+  uint16_t* const s_tr = s_trans[wave];
   const int r = lane & 31, h = lane >> 5;
   for (int x = tid; x < NB * KS2 * WAVE; x += blockDim.x) s_w2[x] = p.w2f[x];
   for (int x = tid; x < 2 * MLP_HID + 32; x += blockDim.x) s_b[x] = p.bias[x];
@@ -195,8 +223,6 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
   for (int64_t tl = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave; tl < ntiles; tl += nw) {
     const int64_t m = tl * 32 + r;  // this lane's row (state)
     const bool ok = m < p.M;
-    const int64_t Mp = p.Mpad;
-    const int64_t cb = (int64_t)(4 * h) * Mp + m;  // (unit 4h, row m) of a unit-major array
     // ---- X^T fragments (B operand of layer 1), stored for dW1 ----
     bf16x8 xf[KS1];
     {
@@ -208,11 +234,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       }
     }
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) {
-      const u32x4_ d = __builtin_bit_cast(u32x4_, xf[s]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) p.xT[(int64_t)(16 * s + 8 * h + j) * Mp + m] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
-    }
+    for (int s = 0; s < KS1; ++s) store_rows(p.xT, MLP_IN, 16 * s, tl, xf[s], s_tr, lane, o_lin);
     // ---- layer 1: H1^T = relu(bf16(W1^T X^T + b1)) ----
     bf16x8 h1[KS2];
 #pragma unroll
@@ -222,8 +244,8 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       for (int s = 0; s < KS1; ++s) c = mfma(frag(r1, l16, n * KS1 + s), xf[s], c);
       h1[2 * n] = relu_pack(c, 0);
       h1[2 * n + 1] = relu_pack(c, 1);
-      store_frag(p.h1T + cb, Mp, 2 * n, h1[2 * n]);
-      store_frag(p.h1T + cb, Mp, 2 * n + 1, h1[2 * n + 1]);
+      store_rows(p.h1T, MLP_HID, 32 * n, tl, h1[2 * n], s_tr, lane, o_kin);
+      store_rows(p.h1T, MLP_HID, 32 * n + 16, tl, h1[2 * n + 1], s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- layer 2: H2^T = relu(bf16(W2^T H1^T + b2)); layer 3: Y^T = W3^T H2^T + b3 ----
@@ -236,8 +258,8 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       for (int kk = 0; kk < KS2; ++kk) c = mfma(s_w2[(n * KS2 + kk) * WAVE + lane], h1[kk], c);
       h2[2 * n] = relu_pack(c, 0);
       h2[2 * n + 1] = relu_pack(c, 1);
-      store_frag(p.h2T + cb, Mp, 2 * n, h2[2 * n]);
-      store_frag(p.h2T + cb, Mp, 2 * n + 1, h2[2 * n + 1]);
+      store_rows(p.h2T, MLP_HID, 32 * n, tl, h2[2 * n], s_tr, lane, o_kin);
+      store_rows(p.h2T, MLP_HID, 32 * n + 16, tl, h2[2 * n + 1], s_tr, lane, o_kin);
       yv = mfma(frag(r3, l16, 2 * n), h2[2 * n], yv);
       yv = mfma(frag(r3, l16, 2 * n + 1), h2[2 * n + 1], yv);
       __builtin_amdgcn_sched_barrier(0);
@@ -271,10 +293,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
     for (int w = 0; w < 4; ++w)
       gw[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){g8[2 * w], g8[2 * w + 1]}, bf16x2v));
     const bf16x8 gyf = __builtin_bit_cast(bf16x8, gw);
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) p.gyT[(int64_t)j * Mp + m] = (uint16_t)(gw[j >> 1] >> (16 * (j & 1)));
-    }
+    store_rows(p.gyT, MLP_OUT, 0, tl, gyf, s_tr, lane, o_lin);  // half 1 holds zeros (units 8..15, not stored)
     __builtin_amdgcn_sched_barrier(0);
     // ---- dH2^T = (W3 g_y^T) masked by H2 > 0 (H2 dies here) ----
     bf16x8 dh2[KS2];
@@ -283,8 +302,8 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       const f32x16 c = mfma(frag(r3b, l16, n), gyf, zero16());
       dh2[2 * n] = mask_pack(c, 0, h2[2 * n]);
       dh2[2 * n + 1] = mask_pack(c, 1, h2[2 * n + 1]);
-      store_frag(p.dh2T + cb, Mp, 2 * n, dh2[2 * n]);
-      store_frag(p.dh2T + cb, Mp, 2 * n + 1, dh2[2 * n + 1]);
+      store_rows(p.dh2T, MLP_HID, 32 * n, tl, dh2[2 * n], s_tr, lane, o_kin);
+      store_rows(p.dh2T, MLP_HID, 32 * n + 16, tl, dh2[2 * n + 1], s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- dH1^T = (W2 dH2^T) masked by H1 > 0, one 32-row block at a time ----
@@ -293,50 +312,120 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       f32x16 c = zero16();
 #pragma unroll
       for (int kk = 0; kk < KS2; ++kk) c = mfma(frag(r2b, l16, n * KS2 + kk), dh2[kk], c);
-      store_frag(p.dh1T + cb, Mp, 2 * n, mask_pack(c, 0, h1[2 * n]));
-      store_frag(p.dh1T + cb, Mp, 2 * n + 1, mask_pack(c, 1, h1[2 * n + 1]));
+      store_rows(p.dh1T, MLP_HID, 32 * n, tl, mask_pack(c, 0, h1[2 * n]), s_tr, lane, o_kin);
+      store_rows(p.dh1T, MLP_HID, 32 * n + 16, tl, mask_pack(c, 1, h1[2 * n + 1]), s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// C[a][b] = sum_m A[a][m] B[b][m] (A: [KA][Mpad], B: [KB][Mpad] bf16,
-// unit-major; rows beyond KA / KB read as zero). Grid: (32x32 output tiles) x
-// (row splits); each wave accumulates one tile over its rows 16 at a time and
-// writes fp32 partials [split][KA][KB]; pg_reduce_kernel sums the splits in
-// order.
+// C[a][b] = sum_m A[a][m] B[b][m] (A: KA units, B: KB units, row-blocked bf16
+// arrays; units past KA / KB read as zero) and, with q.bpart, the bias
+// gradient sum_m B[b][m] as one more MFMA per column tile against a constant
+// A fragment (row 0 all ones), so the bias never re-reads B. One 8-wave
+// workgroup per CU (q.splits of them; two waves per SIMD) owns a contiguous
+// chunk of rows and the WHOLE output: the (KA/32) x (KB/32) tiles are split
+// into eight wave blocks of RPW x CPW tiles whose fp32 accumulators stay in
+// registers over the chunk, 16 rows per MFMA k-step. An operand fragment is
+// one 1 KB run (lane (r, h): unit r of the slab, rows 8h..8h+7 of the block);
+// the waves' shared fragments come from L1 / L2. Wave (row group g, column
+// group) owns the bias of its column tile g (every column tile once: the
+// instantiations have at least CPW row groups). The next k-step's fragments
+// are in flight during this one's MFMAs. Partials [split][KA][KB] are summed
+// in split order by pg_reduce_kernel (deterministic).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) pg_wgrad_kernel(WgradParams q) {
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int tb = (q.KB + 31) / 32;
-  const int tile = blockIdx.x % (((q.KA + 31) / 32) * tb), split = blockIdx.x / (((q.KA + 31) / 32) * tb);
-  const int a0 = tile / tb * 32, b0 = tile % tb * 32;
+constexpr int WG_WAVES = 8;
+template <int RPW, int CPW>
+__global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams q) {
+  static_assert(RPW * CPW <= 8, "accumulators");
+  // w wave-uniform in an SGPR (the loads' resources and offsets derive from it)
+  const int lane = threadIdx.x & (WAVE - 1), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+  const int r = lane & 31, h = lane >> 5;
+  const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32;
+  const int wc = nct / CPW, wr = nrt / RPW;  // wave blocks per column / row of the tile grid
+  if (w >= wr * wc) return;                 // wave-uniform; no barrier below
+  const int g = w / wc, rt0 = g * RPW, ct0 = (w % wc) * CPW;
   const int64_t chunk = (q.Mpad / 16 + q.splits - 1) / q.splits * 16;
-  const int64_t m0 = (int64_t)split * chunk, m1 = min(m0 + chunk, q.Mpad);
-  const bool va = a0 + r < q.KA, vb = b0 + r < q.KB;
-  const bf16x8* pa = reinterpret_cast<const bf16x8*>(q.A + (int64_t)(va ? a0 + r : 0) * q.Mpad + 8 * h);
-  const bf16x8* pb = reinterpret_cast<const bf16x8*>(q.B + (int64_t)(vb ? b0 + r : 0) * q.Mpad + 8 * h);
+  // (a split past the last row still writes its zero partials)
+  const int64_t m0 = min((int64_t)blockIdx.x * chunk, q.Mpad), m1 = min(m0 + chunk, q.Mpad);
+  const int jb = q.bpart && g < CPW ? g : -1;  // the bias tile: column tile ct0 + jb
   const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-  f32x16 c = zero16();
-  int64_t m = m0;
-  for (; m + 64 <= m1; m += 64) {  // four k-steps in flight
-    bf16x8 x[4], y[4];
+  const short one = 0x3F80;  // bf16 1.0
+  const bf16x8 ones = r == 0 ? bf16x8{one, one, one, one, one, one, one, one} : z;
+  // one buffer resource per operand over this chunk's row blocks (base and
+  // size through readfirstlane: a resource word the compiler left in a VGPR
+  // would turn every load into a waterfall loop); a lane whose unit is past
+  // KA / KB reads out of range (zero)
+  auto chunk_rsrc = [&](const uint16_t* base, int U) {
+    const uint64_t a = (uint64_t)(base + (m0 >> 4) * U * 16);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(((m1 - m0) >> 4) * U * 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rsa = chunk_rsrc(q.A, q.KA), rsb = chunk_rsrc(q.B, q.KB);
+  int oa[RPW], ob[CPW];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x[k] = va ? pa[(m + 16 * k) / 8] : z;
-      y[k] = vb ? pb[(m + 16 * k) / 8] : z;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) c = mfma(x[k], y[k], c);
+  for (int i = 0; i < RPW; ++i) {
+    const int u = (rt0 + i) * 32 + r;
+    oa[i] = u < q.KA ? u * 32 + 16 * h : 0x40000000;
   }
-  for (; m < m1; m += 16) c = mfma(va ? pa[m / 8] : z, vb ? pb[m / 8] : z, c);
-  // accumulator register k: row a0 + (k&3) + 8(k>>2) + 4h, column b0 + r
-  float* out = q.part + (int64_t)split * q.KA * q.KB;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int a = a0 + (k & 3) + 8 * (k >> 2) + 4 * h, b = b0 + r;
-    if (a < q.KA && b < q.KB) out[(int64_t)a * q.KB + b] = c[k];
+  for (int j = 0; j < CPW; ++j) {
+    const int u = (ct0 + j) * 32 + r;
+    ob[j] = u < q.KB ? u * 32 + 16 * h : 0x40000000;
+  }
+  const int sa = q.KA * 32, sb = q.KB * 32;  // bytes per row block
+  f32x16 c[RPW][CPW], cb = zero16();
+#pragma unroll
+  for (int i = 0; i < RPW; ++i)
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) c[i][j] = zero16();
+  bf16x8 xa[2][RPW], xb[2][CPW];
+  auto load = [&](int blk, auto S) {  // row block blk of the chunk into buffer S
+#pragma unroll
+    for (int i = 0; i < RPW; ++i)
+      xa[S][i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsa, oa[i], blk * sa, 0));
+#pragma unroll
+    for (int j = 0; j < CPW; ++j)
+      xb[S][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsb, ob[j], blk * sb, 0));
+  };
+  const int nblk = (int)((m1 - m0) >> 4);
+  if (nblk > 0) load(0, std::integral_constant<int, 0>{});
+  if (nblk > 1) load(1, std::integral_constant<int, 1>{});
+  // this k-step's fragments in buffer S, the next one's in flight in 1 - S;
+  // buffer S is refilled (two k-steps ahead) once its MFMAs have read it. Two
+  // k-steps per trip keep the buffer index a compile-time constant (a
+  // runtime-indexed register array would live in scratch memory)
+  auto kstep = [&](int blk, auto S) {
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) c[i][j] = mfma(xa[S][i], xb[S][j], c[i][j]);
+      if (j == jb) cb = mfma(ones, xb[S][j], cb);  // wave-uniform branch
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (blk + 2 < nblk) load(blk + 2, S);
+  };
+  for (int blk = 0; blk < nblk; blk += 2) {
+    kstep(blk, std::integral_constant<int, 0>{});
+    if (blk + 1 < nblk) kstep(blk + 1, std::integral_constant<int, 1>{});
+  }
+  // accumulator register k: row a0 + (k&3) + 8(k>>2) + 4h, column b0 + r
+  float* out = q.part + (int64_t)blockIdx.x * q.KA * q.KB;
+#pragma unroll
+  for (int i = 0; i < RPW; ++i)
+#pragma unroll
+    for (int j = 0; j < CPW; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int a = (rt0 + i) * 32 + (k & 3) + 8 * (k >> 2) + 4 * h, b = (ct0 + j) * 32 + r;
+        if (a < q.KA && b < q.KB) out[(int64_t)a * q.KB + b] = c[i][j][k];
+      }
+  if (jb >= 0 && h == 0) {  // row 0 of the bias tile: register 0 of the lower half
+    const int b = (ct0 + jb) * 32 + r;
+    if (b < q.KB) q.bpart[(int64_t)blockIdx.x * q.KB + b] = cb[0];
   }
 }
 
@@ -364,11 +453,19 @@ hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_pg_wgrad(const WgradParams& q, float* out, hipStream_t s) {
-  const int tiles = ((q.KA + 31) / 32) * ((q.KB + 31) / 32);
-  hipLaunchKernelGGL(pg_wgrad_kernel, dim3((unsigned)(tiles * q.splits)), dim3(64), 0, s, q);
+hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, hipStream_t s) {
+  // eight wave blocks over the output tiles
+  const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32;
+  const dim3 grid((unsigned)q.splits), block(64 * WG_WAVES);
+  if (nrt == 8 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 4>), grid, block, 0, s, q);       // dW2 (+ db2)
+  else if (nrt == 2 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 1>), grid, block, 0, s, q);  // dW1 (+ db1)
+  else if (nrt == 8 && nct == 1) hipLaunchKernelGGL((pg_wgrad_kernel<1, 1>), grid, block, 0, s, q);  // dW3 (+ db3)
+  else return hipErrorInvalidValue;
   const int64_t n = (int64_t)q.KA * q.KB;
   hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q.part, out, n, q.splits);
+  if (q.bpart && out_bias)
+    hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((q.KB + 255) / 256)), dim3(256), 0, s, q.bpart, out_bias,
+                       (int64_t)q.KB, q.splits);
   return hipGetLastError();
 }
 

@@ -645,6 +645,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   // ---- per-scenario parameters ----
   const double cw = active && p.cw ? p.cw[i] : gw->carbon_weight;
   double wc1000 = cw * 1000.0;  // the fused closed loop sets it every step
+  int pwi = 0;                  // ... and its argmin-table weight index (16 * weight)
   const int reset_ca = active && p.reset_ca ? (int)p.reset_ca[i] : gw->reset_ca_s;
   const int pswitch = active && p.pswitch ? (int)p.pswitch[i] : gw->peak_switch;
 
@@ -972,6 +973,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         for (int d = 0; d < DMAX; ++d)
           if (d < D && dep[d].scaler == CCKA_SCALER_HPA) target[d] = tg;
         wc1000 = c * 1000.0;
+        pwi = (int)(c * 16.0);
         if (p.rec_target) {
           p.rec_target[(int64_t)t * p.N + i] = (int16_t)tg;
           p.rec_cw[(int64_t)t * p.N + i] = c;
@@ -1269,8 +1271,69 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       }
     }
 
-    // ---- F2. Karpenter provisioning, wave-cooperative ----
-    {
+    // ---- F2. Karpenter provisioning ----
+    if (POL > 0 && p.ptable) {
+      // the fused closed loop on a single-deployment world without pool limits:
+      // claims of min(J, pending) pods in slot order from the first pool (in
+      // Karpenter's order) whose capacity types the deployment admits and
+      // whose J (largest pod count any offered type holds) is > 0, each launch
+      // one read of the argmin table (table_kernel: region-hour, zone mask,
+      // capacity mask, carbon weight, pods) -- the same choice as the
+      // wave-cooperative scans below, lane-local (rollout_d1_kernel's F2)
+      uint32_t fm = ~used & slot_mask;
+      int pd = pend[0];
+      if (active && pd > 0 && fm && !(p.ablate & 2)) {
+        const int rh = my_r * 24 + hour;
+        int q = -1, J = 0, zi = 0;
+        uint32_t cm = 0;
+        for (int qq = 0; qq < NP && q < 0; ++qq) {
+          const uint32_t c = pcm[qq] & capsel[0];
+          const int z = c ? p.pzmi[pzm[qq] & 15] : -1;
+          const int j = z >= 0 ? p.pjtab[(rh * p.pNZI + z) * 3 + (int)(c - 1)] : 0;
+          if (j > 0) { q = qq; J = j; cm = c; zi = z; }
+        }
+        if (q >= 0) {
+          const int2* row = p.ptable + ((((int64_t)rh * p.pNZI + zi) * 3 + (cm - 1)) * p.pNW + pwi) * p.pJT;
+          while (pd > 0 && fm) {
+            const int slot = __ffs((int)fm) - 1;
+            fm &= fm - 1;
+            const int k = min(J, pd);
+            const int2 e = row[k];  // never empty: k <= J
+            const int price = e.x, bk = e.y & 1023, bz = e.y >> 10 & 3, bc = e.y >> 12 & 1, cap = e.y >> 16;
+            const bool now_ready = delay == 0;
+#pragma unroll
+            for (int n = 0; n < MAXN; ++n) {
+              if (n == slot) {
+                ninfo[n] = ni_make(q, bk, bz, bc);
+                nready[n] = t + delay;
+                nlast[n] = t;
+                nprice[n] = price;
+                ncap[n] = cap;
+                npods[n][0] = k;
+              }
+            }
+            placed[0] += k;
+            if (now_ready) rpods[0] += k;
+            used |= 1u << slot;
+            if (now_ready) rdy |= 1u << slot;
+            else next_ready = min(next_ready, t + delay);
+#pragma unroll
+            for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+              if (qq == q) puse[qq] += L.types[bk].vcpu * 1000;
+            if (bc == 0) nsp++; else nod++;
+            burn += price;
+            launches++;
+            if (det) det->d.pool_launches[q]++;
+            last_choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)q << 16;
+            hash = (hash ^ last_choice) * 16777619u;
+            step_last_type = bk;
+            flags |= 2u;
+            if (now_ready) g_dirty = true;
+            pd -= k;
+          }
+        }
+      }
+    } else {
       int anyp = 0;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) anyp |= pend[d] > 0;

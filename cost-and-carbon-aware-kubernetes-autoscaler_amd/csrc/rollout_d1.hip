@@ -779,9 +779,18 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     tq = upto;
   };
 
-  // load column: the scenario's own trace, or its shared trace (policy sweeps)
-  const int32_t* lp = p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
-  const long long lsl = opq(p.NL);
+  // load column: the scenario's own trace, or its shared trace (policy
+  // sweeps); per-scenario traces are read wave-tiled when the host built that
+  // copy (the wave's rows contiguous: no 128-B line shared with another wave)
+  const int64_t wtb = [&] {  // the wave's first scenario (wave-uniform)
+    const int64_t x = wv * p.lpw;
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(x & 0xffffffffLL));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  }();
+  const int32_t* lp = p.load_w ? p.load_w + wtb * T + lane
+                               : p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
+  const long long lsl = opq(p.load_w ? (long long)min((int64_t)p.lpw, p.N - wtb) : (long long)p.NL);
   // load-sample ring of this wave
   const uint32_t ring_off = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(((uint32_t)p.K * 16u + 255u) / 256u * 256u + (threadIdx.x / WAVE) * (uint32_t)D1_RING_BYTES));
@@ -821,12 +830,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // trajectory records scenario-major on the device ([N][T]: a lane's records
   // are contiguous, so its consecutive steps fill whole lines however far the
   // lanes drift apart); ccka_get_trajectory returns them [T][N]
-  const int64_t w0 = [&] {  // the wave's first scenario (wave-uniform)
-    const int64_t x = wv * p.lpw;
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32));
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(x & 0xffffffffLL));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-  }();
+  const int64_t w0 = wtb;
   const int wlanes = (int)min((int64_t)p.lpw, p.N - w0);
   const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
       traj ? (void*)(reinterpret_cast<int4*>(p.traj) + w0 * T) : (void*)p.load, 0, traj ? wlanes * T * 16 : 0,
@@ -1983,6 +1987,27 @@ hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, in
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(traj_transpose_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                      reinterpret_cast<const int4*>(in), reinterpret_cast<int4*>(out), N, T, t0, tc);
+  return hipGetLastError();
+}
+
+// [T][N] load trace -> wave-tiled [wave][T][lanes] (the single-deployment
+// kernel's read layout: a wave's rows contiguous, lanes = lpw but the last
+// wave's remainder), once per trace / lanes-per-wave change (ccka_abi.cpp
+// d1_trace_tile); reads coalesced, writes in runs of `lanes` ints.
+__global__ void __launch_bounds__(256) trace_tile_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                         int64_t N, int64_t T, int64_t lpw) {
+  const int64_t total = N * T, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
+    const int64_t t = x / N, n = x - t * N;
+    const int64_t w0 = n / lpw * lpw, wl = min(lpw, N - w0);
+    out[w0 * T + t * wl + (n - w0)] = in[x];
+  }
+}
+
+hipError_t launch_trace_tile(const int32_t* in, int32_t* out, int64_t N, int64_t T, int32_t lpw, hipStream_t s) {
+  if (N <= 0 || T <= 0 || lpw <= 0) return hipErrorInvalidValue;
+  const int64_t b0 = (N * T + 255) / 256, blocks = b0 < 65536 ? b0 : 65536;
+  hipLaunchKernelGGL(trace_tile_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, out, N, T, (int64_t)lpw);
   return hipGetLastError();
 }
 

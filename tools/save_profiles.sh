@@ -13,4 +13,11 @@ cp $src/c2_sq_counters.txt "$dst/config2_sq_counters.txt"
 cp $src/stamps.txt "$dst/config2_stamps.txt"
 cp $src/issue/issue.json "$dst/issue_config234.json"
 for f in $src/bench_*.json; do cp "$f" "$dst/"; done
+# tools/refresh_extra.sh: read-traffic split, config-5 kernel traces, loop split
+if [ -d $src/tcc ]; then
+  for d in $src/tcc/*/; do n=$(basename "$d"); cp "$d/run_counter_collection.csv" "$dst/config2_tcc_$n.csv"; done
+fi
+[ -f $src/c5p7/run_kernel_stats.csv ] && cp $src/c5p7/run_kernel_stats.csv "$dst/config5_policy_1e7_kernel_stats.csv"
+[ -f $src/c5g/run_kernel_stats.csv ] && cp $src/c5g/run_kernel_stats.csv "$dst/config5_grad_kernel_stats.csv"
+[ -f $src/loop_split_1e7.txt ] && cp $src/loop_split_1e7.txt "$dst/"
 ls "$dst"
