@@ -1099,6 +1099,8 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     c->last_engine = 2;
     c->traj_nt = true;
   } else {
+    k.ptable = nullptr;  // the argmin-table launches are the policy loops' (weights k / 16)
+    k.pjtab = nullptr;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
     HIPCHK(c, launch_rollout(k, block, lds, c->stream));
@@ -1386,6 +1388,9 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
     }
     return CCKA_OK;
   };
+  // (launches by the wave-cooperative catalog scans: the argmin-table path is
+  // the fused kernel's, whose register budget has room for it)
+  k.ptable = nullptr;
   // graph key: every input of the sequence (parameter blocks by value: their
   // device pointers and sizes)
   std::vector<unsigned char> key;
@@ -1433,6 +1438,8 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   // back to whole-horizon rollouts with the scenarios' own overrides
+  k.ptable = nullptr;
+  k.pjtab = nullptr;
   k.target = c->d_target;
   k.cw = c->d_cw;
   k.state = nullptr;

@@ -128,15 +128,15 @@ __device__ __forceinline__ void store_rows(uint16_t* __restrict__ arr, int U, in
   const u32x4_ d = __builtin_bit_cast(u32x4_, v);
 #pragma unroll
   for (int j = 0; j < 8; ++j) s_tr[o(j, h) * 32 + r] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   const int uu = lane >> 2, rg = lane & 3;
   const u32x4_ w = *reinterpret_cast<const u32x4_*>(s_tr + uu * 32 + 8 * rg);
   if (u0 + uu < U) *reinterpret_cast<u32x4_*>(arr + rb_off(tile * 32 + 8 * rg, U, u0 + uu)) = w;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 // hidden-unit fragment q (the accumulator row order, kin) / input fragment s
 // (units 16 s + 8 h + j) / action fragment (h = 0: actions 0..7)
@@ -223,7 +223,10 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
   for (int64_t tl = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave; tl < ntiles; tl += nw) {
     const int64_t m = tl * 32 + r;  // this lane's row (state)
     const bool ok = m < p.M;
-    // ---- X^T fragments (B operand of layer 1), stored for dW1 ----
+    // Stores trail by one block: a phase's weight fragments for block n are
+    // loaded BEFORE the stores of block n - 1, so waiting for them does not
+    // wait for those stores (vector-memory operations retire in issue order).
+    // ---- X^T fragments (B operand of layer 1), stored for dW1; row factors ----
     bf16x8 xf[KS1];
     {
       const bf16x8* src = reinterpret_cast<const bf16x8*>(p.x + (ok ? m : 0) * MLP_IN + 8 * h);
@@ -233,19 +236,29 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
         xf[s] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
-#pragma unroll
-    for (int s = 0; s < KS1; ++s) store_rows(p.xT, MLP_IN, 16 * s, tl, xf[s], s_tr, lane, o_lin);
+    const float cf = ok ? p.coef[m % p.n_scen] : 0.f;
+    const int act = ok ? (int)p.act[m] : -1;
     // ---- layer 1: H1^T = relu(bf16(W1^T X^T + b1)) ----
     bf16x8 h1[KS2];
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
+      bf16x8 wv[KS1];
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) wv[s] = frag(r1, l16, n * KS1 + s);
+      __builtin_amdgcn_sched_barrier(0);
+      if (n == 0) {
+#pragma unroll
+        for (int s = 0; s < KS1; ++s) store_rows(p.xT, MLP_IN, 16 * s, tl, xf[s], s_tr, lane, o_lin);
+      } else {
+        store_rows(p.h1T, MLP_HID, 32 * (n - 1), tl, h1[2 * n - 2], s_tr, lane, o_kin);
+        store_rows(p.h1T, MLP_HID, 32 * (n - 1) + 16, tl, h1[2 * n - 1], s_tr, lane, o_kin);
+      }
+      __builtin_amdgcn_sched_barrier(0);
       f32x16 c = bias_tile(s_b + 32 * n, h);
 #pragma unroll
-      for (int s = 0; s < KS1; ++s) c = mfma(frag(r1, l16, n * KS1 + s), xf[s], c);
+      for (int s = 0; s < KS1; ++s) c = mfma(wv[s], xf[s], c);
       h1[2 * n] = relu_pack(c, 0);
       h1[2 * n + 1] = relu_pack(c, 1);
-      store_rows(p.h1T, MLP_HID, 32 * n, tl, h1[2 * n], s_tr, lane, o_kin);
-      store_rows(p.h1T, MLP_HID, 32 * n + 16, tl, h1[2 * n + 1], s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- layer 2: H2^T = relu(bf16(W2^T H1^T + b2)); layer 3: Y^T = W3^T H2^T + b3 ----
@@ -253,20 +266,24 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
     f32x16 yv = bias_tile(s_b + 2 * MLP_HID, h);
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
+      const bf16x8 w30 = frag(r3, l16, 2 * n), w31 = frag(r3, l16, 2 * n + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8* prev = n == 0 ? h1 + 2 * (NB - 1) : h2 + 2 * (n - 1);
+      uint16_t* parr = n == 0 ? p.h1T : p.h2T;
+      const int pu = 32 * (n == 0 ? NB - 1 : n - 1);
+      store_rows(parr, MLP_HID, pu, tl, prev[0], s_tr, lane, o_kin);
+      store_rows(parr, MLP_HID, pu + 16, tl, prev[1], s_tr, lane, o_kin);
+      __builtin_amdgcn_sched_barrier(0);
       f32x16 c = bias_tile(s_b + MLP_HID + 32 * n, h);
 #pragma unroll
       for (int kk = 0; kk < KS2; ++kk) c = mfma(s_w2[(n * KS2 + kk) * WAVE + lane], h1[kk], c);
       h2[2 * n] = relu_pack(c, 0);
       h2[2 * n + 1] = relu_pack(c, 1);
-      store_rows(p.h2T, MLP_HID, 32 * n, tl, h2[2 * n], s_tr, lane, o_kin);
-      store_rows(p.h2T, MLP_HID, 32 * n + 16, tl, h2[2 * n + 1], s_tr, lane, o_kin);
-      yv = mfma(frag(r3, l16, 2 * n), h2[2 * n], yv);
-      yv = mfma(frag(r3, l16, 2 * n + 1), h2[2 * n + 1], yv);
+      yv = mfma(w30, h2[2 * n], yv);
+      yv = mfma(w31, h2[2 * n + 1], yv);
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- g_y = c (e_a - softmax(y)): logits 4h..4h+3 of row m in registers 0..3 ----
-    const float cf = ok ? p.coef[m % p.n_scen] : 0.f;
-    const int act = ok ? (int)p.act[m] : -1;
     float mx = fmaxf(fmaxf(yv[0], yv[1]), fmaxf(yv[2], yv[3]));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     float e[4], se = 0.f;
@@ -293,29 +310,49 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
     for (int w = 0; w < 4; ++w)
       gw[w] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){g8[2 * w], g8[2 * w + 1]}, bf16x2v));
     const bf16x8 gyf = __builtin_bit_cast(bf16x8, gw);
-    store_rows(p.gyT, MLP_OUT, 0, tl, gyf, s_tr, lane, o_lin);  // half 1 holds zeros (units 8..15, not stored)
     __builtin_amdgcn_sched_barrier(0);
-    // ---- dH2^T = (W3 g_y^T) masked by H2 > 0 (H2 dies here) ----
+    // ---- dH2^T = (W3 g_y^T) masked by H2 > 0 ----
     bf16x8 dh2[KS2];
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
-      const f32x16 c = mfma(frag(r3b, l16, n), gyf, zero16());
+      const bf16x8 wb = frag(r3b, l16, n);
+      __builtin_amdgcn_sched_barrier(0);
+      if (n == 0) {
+        store_rows(p.h2T, MLP_HID, 32 * (NB - 1), tl, h2[2 * NB - 2], s_tr, lane, o_kin);
+        store_rows(p.h2T, MLP_HID, 32 * (NB - 1) + 16, tl, h2[2 * NB - 1], s_tr, lane, o_kin);
+        store_rows(p.gyT, MLP_OUT, 0, tl, gyf, s_tr, lane, o_lin);  // half 1 holds zeros (units 8..15, not stored)
+      } else {
+        store_rows(p.dh2T, MLP_HID, 32 * (n - 1), tl, dh2[2 * n - 2], s_tr, lane, o_kin);
+        store_rows(p.dh2T, MLP_HID, 32 * (n - 1) + 16, tl, dh2[2 * n - 1], s_tr, lane, o_kin);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const f32x16 c = mfma(wb, gyf, zero16());
       dh2[2 * n] = mask_pack(c, 0, h2[2 * n]);
       dh2[2 * n + 1] = mask_pack(c, 1, h2[2 * n + 1]);
-      store_rows(p.dh2T, MLP_HID, 32 * n, tl, dh2[2 * n], s_tr, lane, o_kin);
-      store_rows(p.dh2T, MLP_HID, 32 * n + 16, tl, dh2[2 * n + 1], s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- dH1^T = (W2 dH2^T) masked by H1 > 0, one 32-row block at a time ----
+    bf16x8 d0 = dh2[2 * NB - 2], d1 = dh2[2 * NB - 1];  // the block stored next
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
+      bf16x8 wv[KS2];
+#pragma unroll
+      for (int kk = 0; kk < KS2; ++kk) wv[kk] = frag(r2b, l16, n * KS2 + kk);
+      __builtin_amdgcn_sched_barrier(0);
+      uint16_t* parr = n == 0 ? p.dh2T : p.dh1T;
+      const int pu = 32 * (n == 0 ? NB - 1 : n - 1);
+      store_rows(parr, MLP_HID, pu, tl, d0, s_tr, lane, o_kin);
+      store_rows(parr, MLP_HID, pu + 16, tl, d1, s_tr, lane, o_kin);
+      __builtin_amdgcn_sched_barrier(0);
       f32x16 c = zero16();
 #pragma unroll
-      for (int kk = 0; kk < KS2; ++kk) c = mfma(frag(r2b, l16, n * KS2 + kk), dh2[kk], c);
-      store_rows(p.dh1T, MLP_HID, 32 * n, tl, mask_pack(c, 0, h1[2 * n]), s_tr, lane, o_kin);
-      store_rows(p.dh1T, MLP_HID, 32 * n + 16, tl, mask_pack(c, 1, h1[2 * n + 1]), s_tr, lane, o_kin);
+      for (int kk = 0; kk < KS2; ++kk) c = mfma(wv[kk], dh2[kk], c);
+      d0 = mask_pack(c, 0, h1[2 * n]);
+      d1 = mask_pack(c, 1, h1[2 * n + 1]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    store_rows(p.dh1T, MLP_HID, 32 * (NB - 1), tl, d0, s_tr, lane, o_kin);
+    store_rows(p.dh1T, MLP_HID, 32 * (NB - 1) + 16, tl, d1, s_tr, lane, o_kin);
   }
 }
 
