@@ -146,6 +146,7 @@ struct ccka_ctx {
   bool pol_graph_off = false;  // ccka_debug_policy_graph(0): launch the sequence directly
   bool pol_fused_off = false;  // ccka_debug_policy_fused(0): the launched loop even where the fused one applies
   bool pol_table_off = false;  // ccka_debug_policy_table(0): the fused loop's catalog scans instead of the tables
+  int64_t pg_chunk = 0;        // ccka_debug_pg_chunk: rows per backward chunk (0: kPgChunkRows)
   int2* d_ptable = nullptr;    // the fused loop's argmin tables (65 policy carbon weights)
   int32_t* d_pjtab = nullptr;
   double* d_pwc = nullptr;
@@ -1464,73 +1465,86 @@ int ccka_policy_rollout(ccka_ctx* c, int32_t trajectory, int32_t record) {
 // rows m = 0..M-1 of x [M][64] bf16 / act [M] / coef[m % n_scen] -> d_pg_grad
 // (dW1 | db1 | dW2 | db2 | dW3 | db3, fp32, the layouts of ccka_mlp_set_weights)
 static constexpr int64_t kGradFloats = 64 * 256 + 256 + 256 * 256 + 256 + 256 * 8 + 8;
+// Rows per backward chunk: the work arrays hold 1,096 bf16 units per row
+// (2.2 KB), so all N*T rows of a large loop do not fit at once (1e7 x 60 would
+// need 1.3 TB). Chunks of kPgChunkRows rows run one after another, each
+// chunk's gradient added to the running sum in chunk order: the result depends
+// only on M, never on the memory available (deterministic); M <= one chunk is
+// the unchunked computation.
+constexpr int64_t kPgChunkRows = 1LL << 23;
+static int64_t pg_chunk_rows(const ccka_ctx* c) { return c->pg_chunk > 0 ? c->pg_chunk : kPgChunkRows; }
+
 static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const float* coef, int64_t n_scen,
                        int64_t M) {
   if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
   if (M < 1 || n_scen < 1) return fail(c, CCKA_EINVAL, "no rows");
-  const int64_t Mpad = (M + 31) / 32 * 32;
   const int64_t rows = 64 + 4 * MLP_HID + 8;  // xT h1T h2T dh1T dh2T gyT
-  if (c->pg_work_count < rows * Mpad) {
+  const int64_t CH = pg_chunk_rows(c);
+  const int64_t cap = (std::min(M, CH) + 31) / 32 * 32;
+  if (c->pg_work_count < rows * cap) {
     dfree(c->d_pg_work);
     c->pg_work_count = 0;
-    if (hipMalloc((void**)&c->d_pg_work, (size_t)(rows * Mpad) * 2) != hipSuccess)
-      return fail(c, CCKA_ENOMEM, "policy-gradient work alloc (%lld rows x %lld)", (long long)rows, (long long)Mpad);
-    c->pg_work_count = rows * Mpad;
+    if (hipMalloc((void**)&c->d_pg_work, (size_t)(rows * cap) * 2) != hipSuccess)
+      return fail(c, CCKA_ENOMEM, "policy-gradient work alloc (%lld rows x %lld)", (long long)rows, (long long)cap);
+    c->pg_work_count = rows * cap;
   }
   if (!c->d_pg_grad && hipMalloc((void**)&c->d_pg_grad, (size_t)kGradFloats * 4) != hipSuccess)
     return fail(c, CCKA_ENOMEM, "gradient alloc");
-  uint16_t* xT = c->d_pg_work;
-  uint16_t* h1T = xT + 64 * Mpad;
-  uint16_t* h2T = h1T + MLP_HID * Mpad;
-  uint16_t* dh1T = h2T + MLP_HID * Mpad;
-  uint16_t* dh2T = dh1T + MLP_HID * Mpad;
-  uint16_t* gyT = dh2T + MLP_HID * Mpad;
-  PgRowsParams rp{};
-  rp.x = x;
-  rp.act = act;
-  rp.coef = coef;
-  rp.w1f = c->d_w1f;
-  rp.w2f = c->d_w2f;
-  rp.w3f = c->d_w3f;
-  rp.w2b = c->d_w2b;
-  rp.w3b = c->d_w3b;
-  rp.bias = c->d_mb;
-  rp.xT = xT; rp.h1T = h1T; rp.h2T = h2T; rp.dh1T = dh1T; rp.dh2T = dh2T; rp.gyT = gyT;
-  rp.M = M;
-  rp.Mpad = Mpad;
-  rp.n_scen = n_scen;
-  HIPCHK(c, launch_pg_rows(rp, c->cus, c->stream));
-  // the six reductions over rows; row splits fill the chip, >= 256 rows each,
-  // fixed for a given Mpad (deterministic sums)
   // the three weight-gradient GEMMs over all rows, each with its bias gradient
   // (the row sums of its B operand) folded in: dW1 | db1, dW2 | db2, dW3 | db3
-  struct G { const uint16_t* a; int ka; const uint16_t* b; int kb; int64_t off, boff; };
   const int64_t o_b1 = 64 * 256, o_w2 = o_b1 + 256, o_b2 = o_w2 + 256 * 256, o_w3 = o_b2 + 256, o_b3 = o_w3 + 256 * 8;
-  const G gs[3] = {{xT, 64, dh1T, MLP_HID, 0, o_b1}, {h1T, MLP_HID, dh2T, MLP_HID, o_w2, o_b2},
-                   {h2T, MLP_HID, gyT, MLP_OUT, o_w3, o_b3}};
-  // one workgroup per CU owns a chunk of rows and the whole output (pg.hip);
-  // the split count is fixed for a given Mpad (deterministic sums)
-  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(c->cus, Mpad / 256));
-  int64_t need = 0;
-  for (const G& g : gs) need = std::max<int64_t>(need, (int64_t)splits * (g.ka * g.kb + g.kb));
-  if (c->pg_part_count < need) {
-    dfree(c->d_pg_part);
-    c->pg_part_count = 0;
-    if (hipMalloc((void**)&c->d_pg_part, (size_t)need * 4) != hipSuccess)
-      return fail(c, CCKA_ENOMEM, "gradient partials alloc");
-    c->pg_part_count = need;
-  }
-  for (const G& g : gs) {
-    WgradParams q{};
-    q.A = g.a;
-    q.B = g.b;
-    q.part = c->d_pg_part;
-    q.bpart = c->d_pg_part + (int64_t)splits * g.ka * g.kb;
-    q.Mpad = Mpad;
-    q.KA = g.ka;
-    q.KB = g.kb;
-    q.splits = splits;
-    HIPCHK(c, launch_pg_wgrad(q, c->d_pg_grad + g.off, c->d_pg_grad + g.boff, c->stream));
+  for (int64_t r0 = 0; r0 < M; r0 += CH) {
+    const int64_t Mc = std::min(CH, M - r0);
+    const int64_t Mpad = (Mc + 31) / 32 * 32;
+    uint16_t* xT = c->d_pg_work;
+    uint16_t* h1T = xT + 64 * Mpad;
+    uint16_t* h2T = h1T + MLP_HID * Mpad;
+    uint16_t* dh1T = h2T + MLP_HID * Mpad;
+    uint16_t* dh2T = dh1T + MLP_HID * Mpad;
+    uint16_t* gyT = dh2T + MLP_HID * Mpad;
+    PgRowsParams rp{};
+    rp.x = x + r0 * MLP_IN;
+    rp.act = act + r0;
+    rp.coef = coef;
+    rp.w1f = c->d_w1f;
+    rp.w2f = c->d_w2f;
+    rp.w3f = c->d_w3f;
+    rp.w2b = c->d_w2b;
+    rp.w3b = c->d_w3b;
+    rp.bias = c->d_mb;
+    rp.xT = xT; rp.h1T = h1T; rp.h2T = h2T; rp.dh1T = dh1T; rp.dh2T = dh2T; rp.gyT = gyT;
+    rp.M = Mc;
+    rp.Mpad = Mpad;
+    rp.n_scen = n_scen;
+    rp.row0 = r0;
+    HIPCHK(c, launch_pg_rows(rp, c->cus, c->stream));
+    struct G { const uint16_t* a; int ka; const uint16_t* b; int kb; int64_t off, boff; };
+    const G gs[3] = {{xT, 64, dh1T, MLP_HID, 0, o_b1}, {h1T, MLP_HID, dh2T, MLP_HID, o_w2, o_b2},
+                     {h2T, MLP_HID, gyT, MLP_OUT, o_w3, o_b3}};
+    // one workgroup per CU owns a share of the chunk's rows and the whole
+    // output (pg.hip); the split count is fixed for a given Mpad
+    const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(c->cus, Mpad / 256));
+    int64_t need = 0;
+    for (const G& g : gs) need = std::max<int64_t>(need, (int64_t)splits * (g.ka * g.kb + g.kb));
+    if (c->pg_part_count < need) {
+      dfree(c->d_pg_part);
+      c->pg_part_count = 0;
+      if (hipMalloc((void**)&c->d_pg_part, (size_t)need * 4) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "gradient partials alloc");
+      c->pg_part_count = need;
+    }
+    for (const G& g : gs) {
+      WgradParams q{};
+      q.A = g.a;
+      q.B = g.b;
+      q.part = c->d_pg_part;
+      q.bpart = c->d_pg_part + (int64_t)splits * g.ka * g.kb;
+      q.Mpad = Mpad;
+      q.KA = g.ka;
+      q.KB = g.kb;
+      q.splits = splits;
+      HIPCHK(c, launch_pg_wgrad(q, c->d_pg_grad + g.off, c->d_pg_grad + g.boff, r0 > 0 ? 1 : 0, c->stream));
+    }
   }
   return CCKA_OK;
 }
@@ -2237,6 +2251,14 @@ int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
 // Internal: scenarios per wave of the single-deployment kernel (1..64; 0 = automatic).
 // Internal: 0 = enqueue the closed loop's launches directly instead of
 // replaying its captured hipGraph (1, the default)
+// Internal: rows per policy-gradient backward chunk (multiple of 32; 0 = the
+// default 2^23), to exercise the chunked sum at test sizes.
+int ccka_debug_pg_chunk(ccka_ctx* c, int64_t rows) {
+  if (!c || rows < 0 || rows % 32) return CCKA_EINVAL;
+  c->pg_chunk = rows;
+  return CCKA_OK;
+}
+
 // Internal: 0 = the fused loop scans the catalog for its launches (A/B of the
 // argmin tables; same results).
 int ccka_debug_policy_table(ccka_ctx* c, int32_t on) {

@@ -328,7 +328,7 @@ hipError_t launch_policy_sample(const PgSampleParams& q, hipStream_t s);
 struct PgRowsParams {
   const uint16_t* x;        // [M][64] bf16
   const uint8_t* act;       // [M]
-  const float* coef;        // [n_scen]: row m's factor is coef[m % n_scen]
+  const float* coef;        // [n_scen]
   const mlp_bf16x8* w1f;    // forward fragments (as MlpParams)
   const mlp_bf16x8* w2f;
   const mlp_bf16x8* w3f;
@@ -338,6 +338,7 @@ struct PgRowsParams {
   // row-blocked [Mpad/16][64|256|256|256|256|8][16] (element (u, m) at ((m/16) U + u) 16 + m%16)
   uint16_t *xT, *h1T, *h2T, *dh1T, *dh2T, *gyT;
   int64_t M, Mpad, n_scen;
+  int64_t row0;  // global index of row 0 (row chunks): row m's factor is coef[(row0 + m) % n_scen]
 };
 hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s);
 // C[KA][KB] = sum_m A[a][m] B[b][m] over row-blocked bf16 operands (fp32 result)
@@ -350,7 +351,7 @@ struct WgradParams {
   int32_t KA, KB, splits, _pad;
 };
 // out = A B^T summed over rows; out_bias (nullable) = the row sums of B
-hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, hipStream_t s);
+hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, int acc, hipStream_t s);
 hipError_t launch_pg_fill(uint16_t* x, int64_t n, int64_t valid, uint16_t v, hipStream_t s);
 // [N][T] (single-deployment engine, device side) -> steps [t0, t0 + tc) of the
 // [T][N] order ccka_get_trajectory returns, into out[tc][N]

@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
         xf[s] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
-    const float cf = ok ? p.coef[m % p.n_scen] : 0.f;
+    const float cf = ok ? p.coef[(p.row0 + m) % p.n_scen] : 0.f;
     const int act = ok ? (int)p.act[m] : -1;
     // ---- layer 1: H1^T = relu(bf16(W1^T X^T + b1)) ----
     bf16x8 h1[KS2];
@@ -466,13 +466,15 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
   }
 }
 
+// out = sum of the splits' partials in split order (acc: added to out, the
+// running sum over row chunks in chunk order)
 __global__ void __launch_bounds__(256) pg_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                        int64_t n, int splits) {
+                                                        int64_t n, int splits, int acc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float s = 0.f;
   for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
-  out[i] = s;
+  out[i] = acc ? out[i] + s : s;
 }
 
 __global__ void __launch_bounds__(256) pg_fill_kernel(uint16_t* __restrict__ x, int64_t n, int64_t valid, uint16_t v) {
@@ -490,7 +492,7 @@ hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, hipStream_t s) {
+hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, int acc, hipStream_t s) {
   // eight wave blocks over the output tiles
   const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32;
   const dim3 grid((unsigned)q.splits), block(64 * WG_WAVES);
@@ -499,10 +501,10 @@ hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, hi
   else if (nrt == 8 && nct == 1) hipLaunchKernelGGL((pg_wgrad_kernel<1, 1>), grid, block, 0, s, q);  // dW3 (+ db3)
   else return hipErrorInvalidValue;
   const int64_t n = (int64_t)q.KA * q.KB;
-  hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q.part, out, n, q.splits);
+  hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q.part, out, n, q.splits, acc);
   if (q.bpart && out_bias)
     hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((q.KB + 255) / 256)), dim3(256), 0, s, q.bpart, out_bias,
-                       (int64_t)q.KB, q.splits);
+                       (int64_t)q.KB, q.splits, acc);
   return hipGetLastError();
 }
 

@@ -67,6 +67,38 @@ def test_mlp_backward_matches_torch_autograd(engine, m):
         assert e <= 2e-2, f"{k}: relative error {e:.3e}"
 
 
+@pytest.mark.parametrize("chunk", [4096, 32 * 37])
+def test_mlp_backward_row_chunks(engine, chunk):
+    """Row chunks (the backward of N*T rows too many for one work buffer runs
+    in chunks of 2^23 rows, each chunk's gradient added in chunk order): with a
+    small chunk size forced, 20,000 rows in 5 / 17 chunks give the autograd
+    gradient within the same bf16 tolerance and the unchunked kernel's within
+    fp32 summation-order rounding; repeated runs are bit-identical."""
+    import ctypes as C
+    rng = np.random.default_rng(7)
+    m = 20000
+    ws, bs = configs.mlp_weights(11)
+    wb = [configs.to_bf16_bits(w) for w in ws]
+    engine.mlp_set_weights(wb, bs)
+    x = configs.to_bf16_bits(rng.standard_normal((m, 64)).astype(np.float32))
+    act = rng.integers(0, 8, size=m).astype(np.uint8)
+    coef = rng.standard_normal(m).astype(np.float32) / m
+    whole = engine.mlp_backward(x, act, coef)
+    fn = engine.lib.ccka_debug_pg_chunk
+    fn.argtypes = [C.c_void_p, C.c_int64]
+    assert fn(engine.ctx, chunk) == 0
+    try:
+        got = engine.mlp_backward(x, act, coef)
+        again = engine.mlp_backward(x, act, coef)
+    finally:
+        fn(engine.ctx, 0)
+    want = torch_grads(x, act, coef, wb, bs)
+    for k in want:
+        assert rel_err(got[k], want[k]) <= 2e-2, k
+        assert rel_err(got[k], whole[k]) <= 1e-5, k
+        assert np.array_equal(got[k], again[k]), k
+
+
 def test_mlp_backward_single_row_structure(engine):
     """One row with coef 1: every gradient is a rank-1 outer product; a
     fragment or k-order error would break it far beyond bf16 rounding."""

@@ -7,6 +7,8 @@
 # trace). Output: gpurun_out/r2b/ (tools/save_profiles.sh copies it).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/r2b; mkdir -p $out/tcc
+tools/gpu_step.sh pgt 300 python -u -m pytest tests/test_gpu_pg.py tests/test_policy_rollout.py -m gpu -x -q \
+  --timeout 120 --timeout-method thread || exit $?
 pmc() {  # <name> <counters> [bench args]: one PMC pass over one config-2 rollout
   local name="$1" set="$2"; shift 2
   timeout -s KILL 120 rocprofv3 --pmc $set -d "$out/tcc/$name" -o run --output-format csv -- \
@@ -34,6 +36,8 @@ timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$out/c5g" -o run --outp
   python3 bench.py --config 5 --mode grad --steps 3 --warmup 1 --no-cpu > "$out/c5g.log" 2>&1 || exit $?
 tools/gpu_step.sh b5g 300 python bench.py --config 5 --mode grad || exit $?
 grep '^{' gpurun_out/b5g.log | tail -1 > $out/bench_config5_grad.json || exit 1
+tools/gpu_step.sh b5g7 400 python bench.py --config 5 --mode grad --n 10000000 --steps 2 --warmup 1 || exit $?
+grep '^{' gpurun_out/b5g7.log | tail -1 > $out/bench_config5_grad_1e7.json || exit 1
 tools/gpu_step.sh lsplit 300 python tools/loop_split.py 10000000 60 || exit $?
 cp gpurun_out/lsplit.log $out/loop_split_1e7.txt
 echo extra-done
