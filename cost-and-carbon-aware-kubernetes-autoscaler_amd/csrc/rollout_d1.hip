@@ -539,13 +539,23 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   int sready[MAXN], slc[MAXN], scas[MAXN], spods[MAXN], sprice[MAXN], scap[MAXN];
   uint32_t sdyn[MAXN];  // dyn_nw_per_m of the slot's type (SEMANTICS §3.H)
   int salloc[MAXN];     // alloc_cpu_m of the slot's type (< 2^24 by eligibility)
-  int sallocr[MAXN];    // salloc once the node is ready, else 0
+  int sallocr[MAXN];    // salloc once the node is ready, else 0 (read through alloc_ready)
 #pragma unroll
   for (int n = 0; n < MAXN; ++n) {
     sinfo[n] = 0; sready[n] = 0; slc[n] = 0; scas[n] = 0; spods[n] = 0; sprice[n] = 0; scap[n] = 0;
     sdyn[n] = 0; salloc[n] = 0; sallocr[n] = 0;
   }
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
+  // allocatable CPU of slot n if ready, else 0: the one-decision-per-step
+  // instantiations keep it in sallocr (deriving it measured 1-8 % slower
+  // there, DRIFT included); the 15 s-sync ones derive it from `rdy`, so sallocr
+  // is dead there (8 registers: spills 80 -> 44 B and 44 -> 16 B, the
+  // upstream-defaults line 2.90 -> 2.61 ms)
+  constexpr bool kAllocR = NSUB == 1;
+  auto alloc_ready = [&](int n) -> uint32_t {
+    if constexpr (kAllocR) return (uint32_t)sallocr[n];
+    else return (rdy >> n & 1u) ? (uint32_t)salloc[n] : 0u;
+  };
   // DRIFT (SEMANTICS 3.G0): drifted slots, sources of an in-flight pre-spun
   // replacement and those replacements (tainted karpenter.sh/disrupted: no
   // pods placed on them, no consolidation; a replacement's source is
@@ -742,7 +752,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       unsigned long long ed = 0;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        const uint32_t use = min((uint32_t)spods[n] * (uint32_t)upp, (uint32_t)sallocr[n]);  // both uint32: v_min_u32
+        const uint32_t use = min((uint32_t)spods[n] * (uint32_t)upp, alloc_ready(n));  // both uint32: v_min_u32
         ed += (unsigned long long)sdyn[n] * use;
       }
       return (long long)ed;
@@ -751,7 +761,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
     for (int n = 0; n < MAXN; ++n) {
       const uint64_t prod = (uint64_t)(uint32_t)spods[n] * (uint64_t)(uint32_t)upp;
-      const uint32_t al = (uint32_t)sallocr[n];
+      const uint32_t al = alloc_ready(n);
       const uint32_t use = prod < (uint64_t)al ? (uint32_t)prod : al;
       e += (long long)((uint64_t)sdyn[n] * use);
     }

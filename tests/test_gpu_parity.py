@@ -260,6 +260,39 @@ def test_d1_edge_cases(engine, variant):
     compare(rg, rc, tg, tc)
 
 
+def test_d1_trace_layouts(engine):
+    """The single-deployment kernel reads its wave-tiled trace copy
+    ([wave][T][lanes], built at gen_load / set_load); the [T][N] trace
+    (ccka_debug_trace_flat) and a re-tiling after the lanes-per-wave value
+    changes under a resident trace give the same bit-exact results and
+    trajectories as the oracle."""
+    import ctypes as C
+
+    spec = configs.config2_world(n_steps=301)
+    n = 3001
+    sc = configs.hpa_scenarios(n, 5)
+    load = po.gen_load(configs.trace_gen(9), spec.n_steps, 1, n, first_id=5)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    fl = engine.lib.ccka_debug_trace_flat
+    fl.argtypes = [C.c_void_p, C.c_int32]
+    lp = engine.lib.ccka_debug_lpw
+    lp.argtypes = [C.c_void_p, C.c_int32]
+    rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+    assert engine.last_engine()[0] == 2
+    compare(rg, rc, tg, tc)
+    try:
+        assert fl(engine.ctx, 1) == 0
+        engine.rollout(trajectory=True)
+        compare(engine.results(), rc, engine.trajectory(), tc)
+        assert fl(engine.ctx, 0) == 0
+        assert lp(engine.ctx, 23) == 0  # the copy was tiled for the automatic value: re-tiled at the rollout
+        engine.rollout(trajectory=True)
+        compare(engine.results(), rc, engine.trajectory(), tc)
+    finally:
+        fl(engine.ctx, 0)
+        lp(engine.ctx, 0)
+
+
 @pytest.mark.parametrize("lpw,steps", [(1, 97), (7, 5), (17, 29), (33, 1440), (64, 300), (49, 61)])
 def test_d1_lane_skew_schedule(engine, lpw, steps):
     """The lane-skewed schedule of rollout_d1_kernel (quiet steps per lane,

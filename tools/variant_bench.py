@@ -1,7 +1,9 @@
 """Timing of kernel variants (tools/build_variants.py) on the config-2
 trajectory rollout, interleaved rounds in one process; every variant's
 results must equal the main build's bit for bit. Profiling aid only.
-usage: python tools/variant_bench.py [variant names...]"""
+WORLD=defaults: the config-2 world with every upstream default of the path
+(15 s HPA sync, drift, replacement and multi-node consolidation).
+usage: [WORLD=defaults] python tools/variant_bench.py [variant names...]"""
 import glob
 import os
 import sys
@@ -25,7 +27,10 @@ for n, path, lp in libs:
     e = Engine(0, lib_path=path)
     e.lib.ccka_debug_lpw.argtypes = [C.c_void_p, C.c_int32]
     e.lib.ccka_debug_lpw(e.ctx, lp)
-    e.set_world(configs.config2_world())
+    w = configs.config2_world()
+    if os.environ.get("WORLD") == "defaults":
+        w.hpa_sync_s, w.drift, w.replace, w.multi = 15, 1, 1, 1
+    e.set_world(w)
     e.set_scenarios(configs.hpa_scenarios(100_000))
     e.gen_load(configs.trace_gen())
     engs[n] = e
