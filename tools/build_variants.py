@@ -3,6 +3,7 @@ rollout_d1.hip: D1_S_V quiet steps per iteration, D1_K_V event cadence,
 D1_VMN_V trace rows in flight, D1_LEAN_V default-behavior quiet path, D1_NT_V /
 D1_NTL_V streaming hints) as separate libccka.so copies under csrc/build/variants/<name>/,
 linked with the main build's other objects. Profiling aid only.
+NAME=r@other.hip replaces rollout.hip (the general kernel) instead.
 usage: python tools/build_variants.py name=-DD1_S_V=3 [name2="-DA -DB" ...]"""
 import os
 import subprocess
@@ -16,17 +17,20 @@ subprocess.run(["make", "-s", "-C", CSRC], check=True)
 procs = []
 for arg in sys.argv[1:]:
     name, _, defs = arg.partition("=")
-    src = "rollout_d1.hip"
+    src, base, extra = "rollout_d1.hip", "rollout_d1.o", []
+    if defs.startswith("r@"):  # the general kernel's source (built with the MLP flags, as the Makefile does)
+        defs, base, extra = defs[1:], "rollout.o", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
     if defs.startswith("@"):  # NAME=@other.hip[:flags]: another source file in csrc/ (e.g. a committed version)
         src, _, defs = defs[1:].partition(":")
     out = os.path.join(CSRC, "build", "variants", name)
     os.makedirs(out, exist_ok=True)
-    obj = os.path.join(out, "rollout_d1.o")
-    procs.append((name, out, obj, subprocess.Popen(["/opt/rocm/bin/hipcc", *FLAGS, *defs.split(), "-c", "-o", obj,
-                                                    os.path.join(CSRC, src)])))
+    obj = os.path.join(out, base)
+    procs.append((name, out, obj, subprocess.Popen(["/opt/rocm/bin/hipcc", *FLAGS, *extra, *defs.split(), "-c", "-o",
+                                                    obj, os.path.join(CSRC, src)])))
 for name, out, obj, p in procs:
     assert p.wait() == 0, name
-    others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "sweep.o", "mlp.o", "pg.o", "ccka_abi.o")]
+    others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "rollout_d1.o", "sweep.o", "mlp.o", "pg.o",
+                                                       "ccka_abi.o") if f != os.path.basename(obj)]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     os.path.join(out, "libccka.so"), obj, *others, "-L/opt/rocm/lib", "-lrccl",
                     "-Wl,-rpath,/opt/rocm/lib"], check=True)
