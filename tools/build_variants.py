@@ -3,7 +3,7 @@ rollout_d1.hip: D1_S_V quiet steps per iteration, D1_K_V event cadence,
 D1_VMN_V trace rows in flight, D1_LEAN_V default-behavior quiet path, D1_NT_V /
 D1_NTL_V streaming hints) as separate libccka.so copies under csrc/build/variants/<name>/,
 linked with the main build's other objects. Profiling aid only.
-NAME=r@other.hip replaces rollout.hip (the general kernel) instead.
+NAME=r@other.hip replaces rollout.hip (the general kernel) instead, NAME=p@other.hip pg.hip.
 usage: python tools/build_variants.py name=-DD1_S_V=3 [name2="-DA -DB" ...]"""
 import os
 import subprocess
@@ -20,6 +20,8 @@ for arg in sys.argv[1:]:
     src, base, extra = "rollout_d1.hip", "rollout_d1.o", []
     if defs.startswith("r@"):  # the general kernel's source (built with the MLP flags, as the Makefile does)
         defs, base, extra = defs[1:], "rollout.o", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+    elif defs.startswith("p@"):  # the policy-gradient kernels' source
+        defs, base, extra = defs[1:], "pg.o", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
     if defs.startswith("@"):  # NAME=@other.hip[:flags]: another source file in csrc/ (e.g. a committed version)
         src, _, defs = defs[1:].partition(":")
     out = os.path.join(CSRC, "build", "variants", name)
