@@ -116,24 +116,37 @@ __device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
 // per unit and a wgrad operand fragment (32 units x 16 rows) is one 1 KB run.
 __device__ __forceinline__ int64_t rb_off(int64_t m, int U, int u) { return ((m >> 4) * U + u) * 16 + (m & 15); }
 
-// One 16-unit fragment of this wave's 32-row tile into a row-blocked array:
-// lane (row r, half h) holds units o(j, h), j = 0..7, of row r; they go to the
-// wave's 1 KB LDS tile as [unit][row], come back as 8 consecutive rows of one
-// unit per lane (16 B), and each store instruction writes two 512-byte runs
-// (units u0..u0+15 of rows 0-15 and of rows 16-31). Only units < U are stored.
+// One 16-unit fragment of this wave's 32-row tile into a row-blocked array.
+// Lane (row r, half h) holds units o(j, h), j = 0..7, of row r, as two runs of
+// four (o(0..3, h), o(4..7, h)): two 8-byte LDS writes into the wave's
+// [row][unit] image (rows TR_ROW elements apart: 40 B, so the writes of lanes
+// 0-15 hit distinct banks). ds_read_b64_tr_b16 reads it back transposed: lane
+// (group g, i) gets unit i of rows 8g..8g+3 and, with a second read, 8g+4..8g+7
+// (16 B: 8 consecutive rows of one unit), and each store instruction writes
+// two 512-byte runs (units u0..u0+15 of rows 0-15 and of rows 16-31). The read
+// crosses lanes, so every lane takes part (EXEC all ones); only units < U are
+// stored.
+constexpr int TR_ROW = 20;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
 template <class O>
 __device__ __forceinline__ void store_rows(uint16_t* __restrict__ arr, int U, int u0, int64_t tile, const bf16x8& v,
                                            uint16_t* s_tr, int lane, O o) {
   const int r = lane & 31, h = lane >> 5;
   const u32x4_ d = __builtin_bit_cast(u32x4_, v);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s_tr[o(j, h) * 32 + r] = (uint16_t)(d[j >> 1] >> (16 * (j & 1)));
+  *reinterpret_cast<u32x2_*>(s_tr + r * TR_ROW + o(0, h)) = u32x2_{d[0], d[1]};
+  *reinterpret_cast<u32x2_*>(s_tr + r * TR_ROW + o(4, h)) = u32x2_{d[2], d[3]};
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  const int uu = lane >> 2, rg = lane & 3;
-  const u32x4_ w = *reinterpret_cast<const u32x4_*>(s_tr + uu * 32 + 8 * rg);
-  if (u0 + uu < U) *reinterpret_cast<u32x4_*>(arr + rb_off(tile * 32 + 8 * rg, U, u0 + uu)) = w;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const uint16_t* a0 = s_tr + (8 * g + q) * TR_ROW + 4 * pp;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)(a0 + 4 * TR_ROW));
+  const u32x2_ wl = __builtin_bit_cast(u32x2_, lo), wh = __builtin_bit_cast(u32x2_, hi);
+  const u32x4_ w = {wl[0], wl[1], wh[0], wh[1]};
+  if (u0 + i < U) *reinterpret_cast<u32x4_*>(arr + rb_off(tile * 32 + 8 * g, U, u0 + i)) = w;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -208,7 +221,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
   constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
   __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 32];
   __shared__ bf16x8 s_w2[NB * KS2 * WAVE];  // forward W2 fragments, 128 KiB
-  __shared__ __attribute__((aligned(16))) uint16_t s_trans[4][16 * 32];  // per wave: a fragment's [unit][row]
+  __shared__ __attribute__((aligned(16))) uint16_t s_trans[4][32 * TR_ROW];  // per wave: a fragment's [row][unit]
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
   uint16_t* const s_tr = s_trans[wave];
   const int r = lane & 31, h = lane >> 5;
