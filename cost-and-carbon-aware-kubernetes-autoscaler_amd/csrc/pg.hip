@@ -129,24 +129,36 @@ __device__ __forceinline__ int64_t rb_off(int64_t m, int U, int u) { return ((m 
 constexpr int TR_ROW = 20;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2_ __attribute__((ext_vector_type(2)));
-template <class O>
-__device__ __forceinline__ void store_rows(uint16_t* __restrict__ arr, int U, int u0, int64_t tile, const bf16x8& v,
+template <int NF, class O>
+__device__ __forceinline__ void store_rows(uint16_t* __restrict__ arr, int U, int u0, int64_t tile, const bf16x8* v,
                                            uint16_t* s_tr, int lane, O o) {
+  // NF consecutive 16-unit fragments (units u0 + 16 f ...) share one pass: all
+  // writes, one wave barrier, all transposed reads, all stores
   const int r = lane & 31, h = lane >> 5;
-  const u32x4_ d = __builtin_bit_cast(u32x4_, v);
-  *reinterpret_cast<u32x2_*>(s_tr + r * TR_ROW + o(0, h)) = u32x2_{d[0], d[1]};
-  *reinterpret_cast<u32x2_*>(s_tr + r * TR_ROW + o(4, h)) = u32x2_{d[2], d[3]};
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const u32x4_ d = __builtin_bit_cast(u32x4_, v[f]);
+    uint16_t* img = s_tr + f * 32 * TR_ROW;
+    *reinterpret_cast<u32x2_*>(img + r * TR_ROW + o(0, h)) = u32x2_{d[0], d[1]};
+    *reinterpret_cast<u32x2_*>(img + r * TR_ROW + o(4, h)) = u32x2_{d[2], d[3]};
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const uint16_t* a0 = s_tr + (8 * g + q) * TR_ROW + 4 * pp;
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)(a0 + 4 * TR_ROW));
-  const u32x2_ wl = __builtin_bit_cast(u32x2_, lo), wh = __builtin_bit_cast(u32x2_, hi);
-  const u32x4_ w = {wl[0], wl[1], wh[0], wh[1]};
-  if (u0 + i < U) *reinterpret_cast<u32x4_*>(arr + rb_off(tile * 32 + 8 * g, U, u0 + i)) = w;
+  u32x4_ w[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const uint16_t* a0 = s_tr + f * 32 * TR_ROW + (8 * g + q) * TR_ROW + 4 * pp;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)a0);
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(uint32_t)(uintptr_t)(a0 + 4 * TR_ROW));
+    const u32x2_ wl = __builtin_bit_cast(u32x2_, lo), wh = __builtin_bit_cast(u32x2_, hi);
+    w[f] = u32x4_{wl[0], wl[1], wh[0], wh[1]};
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+    if (u0 + 16 * f + i < U) *reinterpret_cast<u32x4_*>(arr + rb_off(tile * 32 + 8 * g, U, u0 + 16 * f + i)) = w[f];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -221,7 +233,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
   constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
   __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 32];
   __shared__ bf16x8 s_w2[NB * KS2 * WAVE];  // forward W2 fragments, 128 KiB
-  __shared__ __attribute__((aligned(16))) uint16_t s_trans[4][32 * TR_ROW];  // per wave: a fragment's [row][unit]
+  __shared__ __attribute__((aligned(16))) uint16_t s_trans[4][4 * 32 * TR_ROW];  // per wave: up to 4 fragments' [row][unit]
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
   uint16_t* const s_tr = s_trans[wave];
   const int r = lane & 31, h = lane >> 5;
@@ -260,11 +272,9 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       for (int s = 0; s < KS1; ++s) wv[s] = frag(r1, l16, n * KS1 + s);
       __builtin_amdgcn_sched_barrier(0);
       if (n == 0) {
-#pragma unroll
-        for (int s = 0; s < KS1; ++s) store_rows(p.xT, MLP_IN, 16 * s, tl, xf[s], s_tr, lane, o_lin);
+        store_rows<KS1>(p.xT, MLP_IN, 0, tl, xf, s_tr, lane, o_lin);
       } else {
-        store_rows(p.h1T, MLP_HID, 32 * (n - 1), tl, h1[2 * n - 2], s_tr, lane, o_kin);
-        store_rows(p.h1T, MLP_HID, 32 * (n - 1) + 16, tl, h1[2 * n - 1], s_tr, lane, o_kin);
+        store_rows<2>(p.h1T, MLP_HID, 32 * (n - 1), tl, h1 + 2 * n - 2, s_tr, lane, o_kin);
       }
       __builtin_amdgcn_sched_barrier(0);
       f32x16 c = bias_tile(s_b + 32 * n, h);
@@ -284,8 +294,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       const bf16x8* prev = n == 0 ? h1 + 2 * (NB - 1) : h2 + 2 * (n - 1);
       uint16_t* parr = n == 0 ? p.h1T : p.h2T;
       const int pu = 32 * (n == 0 ? NB - 1 : n - 1);
-      store_rows(parr, MLP_HID, pu, tl, prev[0], s_tr, lane, o_kin);
-      store_rows(parr, MLP_HID, pu + 16, tl, prev[1], s_tr, lane, o_kin);
+      store_rows<2>(parr, MLP_HID, pu, tl, prev, s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
       f32x16 c = bias_tile(s_b + MLP_HID + 32 * n, h);
 #pragma unroll
@@ -331,12 +340,10 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       const bf16x8 wb = frag(r3b, l16, n);
       __builtin_amdgcn_sched_barrier(0);
       if (n == 0) {
-        store_rows(p.h2T, MLP_HID, 32 * (NB - 1), tl, h2[2 * NB - 2], s_tr, lane, o_kin);
-        store_rows(p.h2T, MLP_HID, 32 * (NB - 1) + 16, tl, h2[2 * NB - 1], s_tr, lane, o_kin);
-        store_rows(p.gyT, MLP_OUT, 0, tl, gyf, s_tr, lane, o_lin);  // half 1 holds zeros (units 8..15, not stored)
+        store_rows<2>(p.h2T, MLP_HID, 32 * (NB - 1), tl, h2 + 2 * NB - 2, s_tr, lane, o_kin);
+        store_rows<1>(p.gyT, MLP_OUT, 0, tl, &gyf, s_tr, lane, o_lin);  // half 1 holds zeros (units 8..15, not stored)
       } else {
-        store_rows(p.dh2T, MLP_HID, 32 * (n - 1), tl, dh2[2 * n - 2], s_tr, lane, o_kin);
-        store_rows(p.dh2T, MLP_HID, 32 * (n - 1) + 16, tl, dh2[2 * n - 1], s_tr, lane, o_kin);
+        store_rows<2>(p.dh2T, MLP_HID, 32 * (n - 1), tl, dh2 + 2 * n - 2, s_tr, lane, o_kin);
       }
       __builtin_amdgcn_sched_barrier(0);
       const f32x16 c = mfma(wb, gyf, zero16());
@@ -345,7 +352,7 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- dH1^T = (W2 dH2^T) masked by H1 > 0, one 32-row block at a time ----
-    bf16x8 d0 = dh2[2 * NB - 2], d1 = dh2[2 * NB - 1];  // the block stored next
+    bf16x8 dd[2] = {dh2[2 * NB - 2], dh2[2 * NB - 1]};  // the block stored next
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
       bf16x8 wv[KS2];
@@ -354,18 +361,16 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
       __builtin_amdgcn_sched_barrier(0);
       uint16_t* parr = n == 0 ? p.dh2T : p.dh1T;
       const int pu = 32 * (n == 0 ? NB - 1 : n - 1);
-      store_rows(parr, MLP_HID, pu, tl, d0, s_tr, lane, o_kin);
-      store_rows(parr, MLP_HID, pu + 16, tl, d1, s_tr, lane, o_kin);
+      store_rows<2>(parr, MLP_HID, pu, tl, dd, s_tr, lane, o_kin);
       __builtin_amdgcn_sched_barrier(0);
       f32x16 c = zero16();
 #pragma unroll
       for (int kk = 0; kk < KS2; ++kk) c = mfma(wv[kk], dh2[kk], c);
-      d0 = mask_pack(c, 0, h1[2 * n]);
-      d1 = mask_pack(c, 1, h1[2 * n + 1]);
+      dd[0] = mask_pack(c, 0, h1[2 * n]);
+      dd[1] = mask_pack(c, 1, h1[2 * n + 1]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    store_rows(p.dh1T, MLP_HID, 32 * (NB - 1), tl, d0, s_tr, lane, o_kin);
-    store_rows(p.dh1T, MLP_HID, 32 * (NB - 1) + 16, tl, d1, s_tr, lane, o_kin);
+    store_rows<2>(p.dh1T, MLP_HID, 32 * (NB - 1), tl, dd, s_tr, lane, o_kin);
   }
 }
 
