@@ -1524,8 +1524,9 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
     // one workgroup per CU owns a share of the chunk's rows and the whole
     // output (pg.hip); the split count is fixed for a given Mpad
     const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(c->cus, Mpad / 256));
-    int64_t need = 0;
-    for (const G& g : gs) need = std::max<int64_t>(need, (int64_t)splits * (g.ka * g.kb + g.kb));
+    // each split's partials in the packed gradient order (w1 | b1 | w2 | b2 |
+    // w3 | b3): one reduction for the three GEMMs
+    const int64_t need = (int64_t)splits * kGradFloats;
     if (c->pg_part_count < need) {
       dfree(c->d_pg_part);
       c->pg_part_count = 0;
@@ -1537,14 +1538,16 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
       WgradParams q{};
       q.A = g.a;
       q.B = g.b;
-      q.part = c->d_pg_part;
-      q.bpart = c->d_pg_part + (int64_t)splits * g.ka * g.kb;
+      q.part = c->d_pg_part + g.off;
+      q.bpart = c->d_pg_part + g.boff;
       q.Mpad = Mpad;
+      q.pstride = kGradFloats;
       q.KA = g.ka;
       q.KB = g.kb;
       q.splits = splits;
-      HIPCHK(c, launch_pg_wgrad(q, c->d_pg_grad + g.off, c->d_pg_grad + g.boff, r0 > 0 ? 1 : 0, c->stream));
+      HIPCHK(c, launch_pg_wgrad(q, c->stream));
     }
+    HIPCHK(c, launch_pg_reduce(c->d_pg_part, c->d_pg_grad, kGradFloats, splits, r0 > 0 ? 1 : 0, c->stream));
   }
   return CCKA_OK;
 }

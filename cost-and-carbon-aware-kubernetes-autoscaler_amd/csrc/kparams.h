@@ -345,13 +345,16 @@ hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s);
 struct WgradParams {
   const uint16_t* A;  // [Mpad/16][KA][16]
   const uint16_t* B;  // [Mpad/16][KB][16]
-  float* part;        // [splits][KA][KB]
-  float* bpart;       // nullable: [splits][KB] column sums of B (the bias gradient)
+  float* part;        // split s's [KA][KB] at part + s * pstride
+  float* bpart;       // nullable: split s's [KB] column sums of B (the bias gradient) at bpart + s * pstride
   int64_t Mpad;
+  int64_t pstride;    // floats between two splits' partials
   int32_t KA, KB, splits, _pad;
 };
-// out = A B^T summed over rows; out_bias (nullable) = the row sums of B
-hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, int acc, hipStream_t s);
+// per-split partials of A B^T summed over the split's rows (+ the row sums of B)
+hipError_t launch_pg_wgrad(const WgradParams& q, hipStream_t s);
+// out[i] (+)= sum over splits of part[s * n + i], in split order
+hipError_t launch_pg_reduce(const float* part, float* out, int64_t n, int splits, int acc, hipStream_t s);
 hipError_t launch_pg_fill(uint16_t* x, int64_t n, int64_t valid, uint16_t v, hipStream_t s);
 // [N][T] (single-deployment engine, device side) -> steps [t0, t0 + tc) of the
 // [T][N] order ccka_get_trajectory returns, into out[tc][N]

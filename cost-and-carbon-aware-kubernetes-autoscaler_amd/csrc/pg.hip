@@ -387,8 +387,9 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
 // the waves' shared fragments come from L1 / L2. Wave (row group g, column
 // group) owns the bias of its column tile g (every column tile once: the
 // instantiations have at least CPW row groups). The next k-step's fragments
-// are in flight during this one's MFMAs. Partials [split][KA][KB] are summed
-// in split order by pg_reduce_kernel (deterministic).
+// are in flight during this one's MFMAs. Each split's partials land in its
+// block of the packed gradient layout; pg_reduce_kernel sums the blocks in
+// split order (deterministic), all three GEMMs in one launch.
 // ---------------------------------------------------------------------------
 constexpr int WG_WAVES = 8;
 template <int RPW, int CPW>
@@ -468,7 +469,7 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
     if (blk + 1 < nblk) kstep(blk + 1, std::integral_constant<int, 1>{});
   }
   // accumulator register k: row a0 + (k&3) + 8(k>>2) + 4h, column b0 + r
-  float* out = q.part + (int64_t)blockIdx.x * q.KA * q.KB;
+  float* out = q.part + (int64_t)blockIdx.x * q.pstride;
 #pragma unroll
   for (int i = 0; i < RPW; ++i)
 #pragma unroll
@@ -480,7 +481,7 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
       }
   if (jb >= 0 && h == 0) {  // row 0 of the bias tile: register 0 of the lower half
     const int b = (ct0 + jb) * 32 + r;
-    if (b < q.KB) q.bpart[(int64_t)blockIdx.x * q.KB + b] = cb[0];
+    if (b < q.KB) q.bpart[(int64_t)blockIdx.x * q.pstride + b] = cb[0];
   }
 }
 
@@ -510,7 +511,7 @@ hipError_t launch_pg_rows(const PgRowsParams& p, int cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, int acc, hipStream_t s) {
+hipError_t launch_pg_wgrad(const WgradParams& q, hipStream_t s) {
   // eight wave blocks over the output tiles
   const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32;
   const dim3 grid((unsigned)q.splits), block(64 * WG_WAVES);
@@ -518,11 +519,11 @@ hipError_t launch_pg_wgrad(const WgradParams& q, float* out, float* out_bias, in
   else if (nrt == 2 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 1>), grid, block, 0, s, q);  // dW1 (+ db1)
   else if (nrt == 8 && nct == 1) hipLaunchKernelGGL((pg_wgrad_kernel<1, 1>), grid, block, 0, s, q);  // dW3 (+ db3)
   else return hipErrorInvalidValue;
-  const int64_t n = (int64_t)q.KA * q.KB;
-  hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q.part, out, n, q.splits, acc);
-  if (q.bpart && out_bias)
-    hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((q.KB + 255) / 256)), dim3(256), 0, s, q.bpart, out_bias,
-                       (int64_t)q.KB, q.splits, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_pg_reduce(const float* part, float* out, int64_t n, int splits, int acc, hipStream_t s) {
+  hipLaunchKernelGGL(pg_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, out, n, splits, acc);
   return hipGetLastError();
 }
 
