@@ -335,9 +335,13 @@ const char* ccka_last_error(const ccka_ctx* ctx);
 int ccka_set_world(ccka_ctx* ctx, const ccka_world* world);
 /* Upload per-scenario parameters (resets any previous batch). */
 int ccka_set_scenarios(ccka_ctx* ctx, const ccka_scenarios* sc);
-/* Upload host load traces, layout [T][D][N] int32. */
+/* Upload host load traces, layout [T][D][N] int32. For a single-deployment
+ * world with per-scenario traces the device also keeps a wave-tiled copy
+ * (another T*N*4 bytes; the single-deployment kernel's read layout, built
+ * here once per trace; without the memory for it that kernel reads [T][N]). */
 int ccka_set_load(ccka_ctx* ctx, const int32_t* load, int64_t count);
-/* Generate load traces on the device (same values as the host generator). */
+/* Generate load traces on the device (same values as the host generator;
+ * the same wave-tiled copy as ccka_set_load). */
 int ccka_gen_load(ccka_ctx* ctx, const ccka_trace_gen* gen);
 /* Copy the device-resident traces back ([T][D][N]). */
 int ccka_get_load(ccka_ctx* ctx, int32_t* load, int64_t count);
