@@ -457,7 +457,11 @@ typedef struct ccka_mlp_grads {
 } ccka_mlp_grads;
 /* One stochastic closed-loop rollout (world, scenarios, load and weights as
  * ccka_policy_rollout; results / actions read back the same way) and the
- * gradient of E[J]; *objective_mean (nullable) = mean J of the batch. */
+ * gradient of E[J]; *objective_mean (nullable) = mean J of the batch.
+ * Device memory: the loop's features, 128 B per (step, scenario) row, plus
+ * the backward's work arrays for one chunk of at most 2^23 rows (2,192 B per
+ * row, ~18 GB); chunks run in order and their gradients add up in that order,
+ * so the result depends on N*T only (1e7 x 60 rows: ~80 GB in all). */
 int ccka_policy_grad(ccka_ctx* ctx, const ccka_pg_params* params, ccka_mlp_grads* out, double* objective_mean);
 /* The sampled action bins [T][N] and the per-scenario factors (J_i - b) / N of
  * the last ccka_policy_grad (count = T*N). */
