@@ -548,10 +548,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   uint32_t used = 0, rdy = 0, cmask = 0;  // cmask: slot capacity type matches the nodeSelector
   // allocatable CPU of slot n if ready, else 0: the one-decision-per-step
   // instantiations keep it in sallocr (deriving it measured 1-8 % slower
-  // there, DRIFT included); the 15 s-sync ones derive it from `rdy`, so sallocr
-  // is dead there (8 registers: spills 80 -> 44 B and 44 -> 16 B, the
-  // upstream-defaults line 2.90 -> 2.61 ms)
-  constexpr bool kAllocR = NSUB == 1;
+  // there, DRIFT included); the 15 s-sync and G3 ones derive it from `rdy`, so
+  // sallocr is dead there (8 registers: spills 80 -> 44 B and 44 -> 16 B, the
+  // upstream-defaults line 2.90 -> 2.61 ms; G3 320 -> 248 B, 7.41 -> 5.72 ms)
+  constexpr bool kAllocR = NSUB == 1 && !G3;
   auto alloc_ready = [&](int n) -> uint32_t {
     if constexpr (kAllocR) return (uint32_t)sallocr[n];
     else return (rdy >> n & 1u) ? (uint32_t)salloc[n] : 0u;

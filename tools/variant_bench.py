@@ -2,7 +2,8 @@
 trajectory rollout, interleaved rounds in one process; every variant's
 results must equal the main build's bit for bit. Profiling aid only.
 WORLD=defaults: the config-2 world with every upstream default of the path
-(15 s HPA sync, drift, replacement and multi-node consolidation).
+(15 s HPA sync, drift, replacement and multi-node consolidation); WORLD=multi50:
+drift, replacement and multi-node consolidation under 50 % budgets (G3).
 usage: [WORLD=defaults] python tools/variant_bench.py [variant names...]"""
 import glob
 import os
@@ -30,6 +31,10 @@ for n, path, lp in libs:
     w = configs.config2_world()
     if os.environ.get("WORLD") == "defaults":
         w.hpa_sync_s, w.drift, w.replace, w.multi = 15, 1, 1, 1
+    if os.environ.get("WORLD") == "multi50":  # multi-node consolidation acting (the G3 instantiation)
+        w.drift, w.replace, w.multi = 1, 1, 1
+        for pool in w.pools:
+            pool.budget_pct = 50
     e.set_world(w)
     e.set_scenarios(configs.hpa_scenarios(100_000))
     e.gen_load(configs.trace_gen())
