@@ -414,6 +414,7 @@ template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = fals
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   static_assert(NSUB == 1 || (NSUB == 4 && BDEF), "15 s sync: lean default path");
   static_assert(HE == 8 || (HE == 4 && NSUB == 1 && BDEF), "4-record ring: default behavior, one decision per step");
+  static_assert(!G3 || (DRIFT && MAXP == 2), "G3: the DRIFT instantiation, two pools");
   constexpr int HW = NSUB == 1 ? HE / 2 : 10;  // history words (2 records each)
   // steps whose records the event step may rebuild: the window's entries
   constexpr int JR = NSUB == 1 ? HE : 5;
@@ -555,6 +556,14 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   auto alloc_ready = [&](int n) -> uint32_t {
     if constexpr (kAllocR) return (uint32_t)sallocr[n];
     else return (rdy >> n & 1u) ? (uint32_t)salloc[n] : 0u;
+  };
+  // consolidateAfter (steps) of slot n's pool: the G3 instantiation derives it
+  // from the pool bits instead of keeping scas[] (8 more registers: its spill
+  // 248 -> 160 B, the multi-node consolidation line 5.69 -> 4.44 ms; in the
+  // 15 s-sync + DRIFT one the same change measured 2 % slower)
+  auto cas_slot = [&](int n) -> int {
+    if constexpr (G3) return casc(cas_of(sinfo[n]));
+    else return scas[n];
   };
   // DRIFT (SEMANTICS 3.G0): drifted slots, sources of an in-flight pre-spun
   // replacement and those replacements (tainted karpenter.sh/disrupted: no
@@ -971,6 +980,9 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         q_peak = peak;
         if (prof != profile) {
           profile = prof;
+          int pold[MAXP];
+#pragma unroll
+          for (int q = 0; q < MAXP; ++q) pold[q] = pcas[q];
 #pragma unroll
           for (int q = 0; q < MAXP; ++q) {
             if (q >= NP) break;
@@ -985,7 +997,14 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
           for (int n = 0; n < MAXN; ++n)
             if (used >> n & 1u) {
               const int c = casc(cas_of(sinfo[n]));
-              slc[n] += c - scas[n];
+              if constexpr (G3) {
+                const int m1 = -(int)(sinfo[n] >> 13 & 1u);
+                // the slot's value before this switch (G3 instantiations have MAXP = 2)
+                const int o = pold[0] ^ ((pold[0] ^ pold[MAXP > 1 ? 1 : 0]) & m1);
+                slc[n] += c - casc(o);
+              } else {
+                slc[n] += c - scas[n];
+              }
               scas[n] = c;
             }
           jchg = true;
@@ -1036,7 +1055,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               excess -= k;
               removed += k;
               if (pass == 1) removed_c += ((cmask & ~taint()) >> n & 1u) ? k : 0;
-              slc[n] = k > 0 ? t + scas[n] : slc[n];
+              slc[n] = k > 0 ? t + cas_slot(n) : slc[n];
             }
             if (pass == 1) { rpods -= removed; Ffree += removed_c; }
           }
@@ -1056,7 +1075,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
               spods[n] += k;
               pd -= k;
               added += k;
-              slc[n] = k > 0 ? t + scas[n] : slc[n];
+              slc[n] = k > 0 ? t + cas_slot(n) : slc[n];
             }
             placed += added;
             if (pass == 0) { rpods += added; Ffree -= added; }
@@ -1264,7 +1283,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                 }
 #pragma unroll
                 for (int n = 0; n < MAXN; ++n)
-                  if (n == m) { spods[n] += got; slc[n] = t + scas[n]; }
+                  if (n == m) { spods[n] += got; slc[n] = t + cas_slot(n); }
                 repm &= ~(1u << m);
                 flags |= 4u;
               }
@@ -1308,7 +1327,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                   const int k = min(fr, need);
                   spods[n] += k;
                   need -= k;
-                  slc[n] = k > 0 ? t + scas[n] : slc[n];
+                  slc[n] = k > 0 ? t + cas_slot(n) : slc[n];
                 }
                 // the rest: a pre-spun replacement under the pool's current
                 // requirements (the F launch rule: the argmin table row), else eviction
@@ -1426,7 +1445,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                     const int k = min(fr, need);
                     spods[n] += k;
                     need -= k;
-                    slc[n] = k > 0 ? t + scas[n] : slc[n];
+                    slc[n] = k > 0 ? t + cas_slot(n) : slc[n];
                   }
                 }
               }
@@ -1558,7 +1577,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
                     for (int n = 0; n < MAXN; ++n) {
                       spods[n] = tp[n];
-                      slc[n] = (touched >> n & 1u) ? t + scas[n] : slc[n];
+                      slc[n] = (touched >> n & 1u) ? t + cas_slot(n) : slc[n];
                       srcmask |= ((set >> n & 1u) && tp[n] > 0 ? 1u : 0u) << n;
                     }
                     uint32_t gone = set & ~srcmask;
