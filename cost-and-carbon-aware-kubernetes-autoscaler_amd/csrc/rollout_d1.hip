@@ -552,10 +552,22 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   // there, DRIFT included); the 15 s-sync and G3 ones derive it from `rdy`, so
   // sallocr is dead there (8 registers: spills 80 -> 44 B and 44 -> 16 B, the
   // upstream-defaults line 2.90 -> 2.61 ms; G3 320 -> 248 B, 7.41 -> 5.72 ms)
+  // per-slot dynamic power and allocatable CPU of the slot's type: the G3
+  // instantiation reads them from the LDS catalog (event paths only) instead
+  // of keeping sdyn[] / salloc[] (16 registers: spill 160 -> 0 B, 244 -> 12 B
+  // with 15 s sync; the multi-node consolidation line 4.50 -> 3.45 ms)
+  auto dyn_of = [&](int n) -> uint32_t {
+    if constexpr (G3) return (uint32_t)s_acc[sinfo[n] & 1023u].z;
+    else return sdyn[n];
+  };
+  auto alloc_of = [&](int n) -> int {
+    if constexpr (G3) return s_acc[sinfo[n] & 1023u].w;
+    else return salloc[n];
+  };
   constexpr bool kAllocR = NSUB == 1 && !G3;
   auto alloc_ready = [&](int n) -> uint32_t {
     if constexpr (kAllocR) return (uint32_t)sallocr[n];
-    else return (rdy >> n & 1u) ? (uint32_t)salloc[n] : 0u;
+    else return (rdy >> n & 1u) ? (uint32_t)alloc_of(n) : 0u;
   };
   // consolidateAfter (steps) of slot n's pool: the G3 instantiation derives it
   // from the pool bits instead of keeping scas[] (8 more registers: its spill
@@ -762,7 +774,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
         const uint32_t use = min((uint32_t)spods[n] * (uint32_t)upp, alloc_ready(n));  // both uint32: v_min_u32
-        ed += (unsigned long long)sdyn[n] * use;
+        ed += (unsigned long long)dyn_of(n) * use;
       }
       return (long long)ed;
     }
@@ -772,7 +784,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
       const uint64_t prod = (uint64_t)(uint32_t)spods[n] * (uint64_t)(uint32_t)upp;
       const uint32_t al = alloc_ready(n);
       const uint32_t use = prod < (uint64_t)al ? (uint32_t)prod : al;
-      e += (long long)((uint64_t)sdyn[n] * use);
+      e += (long long)((uint64_t)dyn_of(n) * use);
     }
     return e;
   };
@@ -1734,8 +1746,8 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
             const uint32_t pr = (rdy >> n & 1u) ? (uint32_t)spods[n] : 0u;
-            sv += (unsigned long long)sdyn[n] * pr;
-            rv = fmaxf(rv, (float)pr * __builtin_amdgcn_rcpf((float)salloc[n]));  // 1/alloc only here
+            sv += (unsigned long long)dyn_of(n) * pr;
+            rv = fmaxf(rv, (float)pr * __builtin_amdgcn_rcpf((float)alloc_of(n)));  // 1/alloc only here
           }
           Ssum = sv;
           Rmax = rv;
