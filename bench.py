@@ -60,6 +60,10 @@ def main():
     ap.add_argument("--multi", action="store_true",
                     help="configs 2-4 with multi-node consolidation (SEMANTICS 3.G3, Karpenter's default for "
                          "WhenEmptyOrUnderutilized pools)")
+    ap.add_argument("--keda", action="store_true",
+                    help="configs 2-3 with a KEDA ScaledObject queue worker instead of the HPA deployment "
+                         "(SURVEY A.2 defaults: scale from / to zero, cooldown 300 s, min 0, max 100; threshold "
+                         "500 per replica, activation 0; docs/SEMANTICS.md 3.C)")
     ap.add_argument("--budget", type=int, default=None,
                     help="NodePool disruption budget in %% of the pool's nodes (default: the reference's 10)")
     ap.add_argument("--hpa-sync", type=int, default=0, choices=[0, 10, 15, 20, 30, 60],
@@ -186,6 +190,9 @@ def main():
             sc = configs.config4_scenarios(rank * grids, grids, ntr)
             gen = configs.config4_trace_gen()
             traj = (args.mode or "summary") == "trajectory"
+        if args.keda:  # the queue-worker side of the path: one ScaledObject per scenario
+            spec.deploys = [configs.deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=500, keda_activation=0,
+                                               keda_cooldown=300, keda_min=0, keda_max=100)]
         spec.drift = int(args.drift)
         spec.replace = int(args.replace)
         spec.multi = int(args.multi)
@@ -316,6 +323,9 @@ def main():
         load_cols = configs.CONFIG4_TRACES if cfg == 4 else N
         bytes_launch = load_cols * T * 4 + (N * T * 16 if traj else 0) + N * 6 + N * 72
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = (None, None) if (args.drift or args.replace or args.multi or args.keda or
+                                                args.hpa_sync not in (0, 60) or args.budget is not None or
+                                                args.trace_flat) else measured_traffic(cfg, traj, N, T)
         workloads = {
             2: "config2: 1e5 clusters x 1 deployment x 1440 one-minute steps, HPA + peak/off-peak, "
                "16-type catalog",
@@ -330,7 +340,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / K * 1e3, "higher_is_better": True,
             "scaling": "strong" if cfg == 3 else "weak", "vs_baseline": None, "dtype": "int32+int64+f64",
             "data": "synthetic (on-device Philox load traces, seed 20251205)",
-            "config": {"workload": workloads[cfg] + (" + Karpenter drift at the zone switch" if args.drift else "")
+            "config": {"workload": (workloads[cfg].replace("HPA", "KEDA ScaledObject (scale to zero)") if args.keda
+                                    else workloads[cfg]) + (" + Karpenter drift at the zone switch" if args.drift else "")
                        + (" + replacement consolidation" if args.replace else "")
                        + (" + multi-node consolidation" if args.multi else "")
                        + (f" + HPA sync every {args.hpa_sync} s" if args.hpa_sync not in (0, 60) else "")
@@ -341,17 +352,18 @@ def main():
                        "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None if args.drift or args.replace or args.multi or args.hpa_sync not in (0, 60)
-                         or args.budget is not None or args.trace_flat
-                         else measured_traffic(cfg, traj, N, T),
-                         "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else "rollout_kernel",
+                         "traffic": traffic,
+                         # not measured in this run: copied from the committed profile named here
+                         "traffic_source": traffic_src,
+                         "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else
+                                   f"rollout_kernel<{len(spec.deploys)},{spec.max_nodes}>",
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},
             # the kernel is issue-bound, not HBM-bound: its measured issue-side
             # utilisation (profiled) and the measured copy ceiling
             # (profiled on the single-deployment kernel only)
             "issue": profiled_issue(cfg) if engine_id == 2 and not (args.drift or args.replace or args.multi or
-                                                                   args.hpa_sync not in (0, 60)) else None,
+                                                                   args.keda or args.hpa_sync not in (0, 60)) else None,
             "totals": {"cost_usd": totals.cost_uphmin / 6e7, "energy_kwh": totals.energy_wmin / 6e4,
                        "gco2_kg": totals.gco2 / 1e3, "slo_minutes": totals.slo_minutes,
                        "launches": totals.launches, "deletions": totals.deletions},
@@ -390,12 +402,15 @@ def measured_traffic(cfg, traj, n, T):
     import glob
 
     if (cfg, n, T) != (2, 100_000, 1440):
-        return None
+        return None, None
     name = "config2_traj_summary.json" if traj else "config2_summary_summary.json"
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*", name)))
     if not paths:
-        return None
-    return json.load(open(paths[-1])).get("traffic_bytes")
+        return None, None
+    d = json.load(open(paths[-1]))
+    return d.get("traffic_bytes"), {"file": os.path.relpath(paths[-1], ROOT), "head": d.get("source_head"),
+                                    "how": "rocprofv3 TCC_EA0 request counters, separate --pmc passes "
+                                           "(tools/prof_round.sh); copied, not measured in this run"}
 
 
 def copy_bandwidth(eng, nbytes=1 << 31, reps=5):
@@ -421,9 +436,12 @@ def profiled_issue(cfg):
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*", "issue_config234.json")))
     if not paths:
         return None
-    d = json.load(open(paths[-1])).get(f"config{cfg}")
+    j = json.load(open(paths[-1]))
+    d = j.get(f"config{cfg}")
     if d:
-        d = dict(d, source=os.path.relpath(paths[-1], ROOT))
+        d = dict(d, issue_source={"file": os.path.relpath(paths[-1], ROOT), "head": j.get("source_head"),
+                                  "how": "rocprofv3 SQ PMC pass (tools/prof_issue.sh); copied, not measured in "
+                                         "this run"})
     return d
 
 

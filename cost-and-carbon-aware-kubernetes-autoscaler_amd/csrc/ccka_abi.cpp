@@ -817,9 +817,10 @@ static int32_t d1_lpw(const ccka_ctx* c) {
 // ([wave][T][lanes]): with [T][N] a wave's 196-byte row shares its first and
 // last 128-byte lines with the neighbouring waves, which run up to hundreds of
 // steps apart (lane skew), so the L2 has evicted those lines before the
-// neighbour reads them. Built once per trace (set_load / gen_load) and lanes-
-// per-wave value, beside the [T][N] trace the other paths read; without the
-// memory for it the kernel reads [T][N] (same results).
+// neighbour reads them. Built lazily by the first single-deployment rollout of
+// a trace and lanes-per-wave value (never by the policy loop or the general
+// kernel, which read [T][N]), beside the [T][N] trace; without the memory for
+// it the kernel reads [T][N] (same results). The policy loop frees it.
 static int d1_trace_tile(ccka_ctx* c) {
   if (!c->d1_world || c->hw.n_deploy != 1 || c->n_traces > 0 || !c->have_load) return CCKA_OK;
   const int32_t lpw = d1_lpw(c);
@@ -852,7 +853,7 @@ int ccka_set_load(ccka_ctx* c, const int32_t* load, int64_t count) {
   HIPCHK(c, hipMemcpyAsync(c->d_load, load, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_load = true;
-  return d1_trace_tile(c);
+  return CCKA_OK;
 }
 
 int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
@@ -880,7 +881,7 @@ int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
   HIPCHK(c, launch_gen_load(gp, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_load = true;
-  return d1_trace_tile(c);
+  return CCKA_OK;
 }
 
 int ccka_get_load(ccka_ctx* c, int32_t* load, int64_t count) {
@@ -1177,8 +1178,13 @@ static int policy_tables(ccka_ctx* c, KParams* k) {
     dfree(c->d_pjtab);
     c->ptable_count = 0;
     if (hipMalloc((void**)&c->d_ptable, (size_t)cnt * sizeof(int2)) != hipSuccess ||
-        hipMalloc((void**)&c->d_pjtab, (size_t)keys * sizeof(int32_t)) != hipSuccess)
-      return fail(c, CCKA_ENOMEM, "policy argmin table alloc (%lld entries)", (long long)cnt);
+        hipMalloc((void**)&c->d_pjtab, (size_t)keys * sizeof(int32_t)) != hipSuccess) {
+      // no memory for the tables: the fused loop scans the catalog instead (same choices)
+      (void)hipGetLastError();
+      dfree(c->d_ptable);
+      dfree(c->d_pjtab);
+      return CCKA_OK;
+    }
     c->ptable_count = cnt;
   }
   if (!c->d_pwc) {
@@ -1212,6 +1218,11 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   if (!c) return CCKA_EINVAL;
   c->pg_valid = false;  // the recorded features / actions are about to be overwritten
   if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
+  // the single-deployment kernel's tiled trace copy (N*T*4 bytes) is not read
+  // here: released for the loop's own arrays, rebuilt by the next rollout
+  dfree(c->d_load_w);
+  c->load_w_count = 0;
+  c->load_w_lpw = 0;
   if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
   if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
   (void)hipSetDevice(c->device);
@@ -1302,21 +1313,28 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
       k.pol_act = pg ? c->d_pg_act : nullptr;
       k.feat_rec = feat_on ? c->d_feat_rec : nullptr;
       k.lds_off_mlp = (int32_t)off;
-      HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+      // the fused-only fields leave the persistent parameter block on every path
+      auto clear_fused = [&]() {
+        k.ptable = nullptr;
+        k.pjtab = nullptr;
+        k.feat = nullptr;
+        k.w1f = k.w2f = k.w3f = nullptr;
+        k.mlp_b = nullptr;
+        k.pol_seed = nullptr;
+        k.rec_target = nullptr;
+        k.rec_cw = nullptr;
+        k.pol_act = nullptr;
+        k.feat_rec = nullptr;
+      };
+      hipError_t le = hipEventRecord(c->ev0, c->stream);
       k.ptable = nullptr;
-      if (!c->pol_table_off && (rc = policy_tables(c, &k)) != CCKA_OK) return rc;
-      HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
-      const hipError_t le = launch_rollout_policy(k, off + mlp_lds, pg ? 2 : 1, c->stream);
-      k.ptable = nullptr;
-      k.pjtab = nullptr;
-      k.feat = nullptr;
-      k.w1f = k.w2f = k.w3f = nullptr;
-      k.mlp_b = nullptr;
-      k.pol_seed = nullptr;
-      k.rec_target = nullptr;
-      k.rec_cw = nullptr;
-      k.pol_act = nullptr;
-      k.feat_rec = nullptr;
+      if (le == hipSuccess && !c->pol_table_off && (rc = policy_tables(c, &k)) != CCKA_OK) {
+        clear_fused();
+        return rc;
+      }
+      if (le == hipSuccess) le = hipEventRecord(c->ev_mid, c->stream);
+      if (le == hipSuccess) le = launch_rollout_policy(k, off + mlp_lds, pg ? 2 : 1, c->stream);
+      clear_fused();
       HIPCHK(c, le);
       HIPCHK(c, hipEventRecord(c->ev1, c->stream));
       c->last_engine = 4;
@@ -1472,6 +1490,7 @@ static constexpr int64_t kGradFloats = 64 * 256 + 256 + 256 * 256 + 256 + 256 * 
 // only on M, never on the memory available (deterministic); M <= one chunk is
 // the unchunked computation.
 constexpr int64_t kPgChunkRows = 1LL << 23;
+constexpr int64_t kPgSplits = 256;  // weight-gradient row splits per chunk (at most)
 static int64_t pg_chunk_rows(const ccka_ctx* c) { return c->pg_chunk > 0 ? c->pg_chunk : kPgChunkRows; }
 
 static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const float* coef, int64_t n_scen,
@@ -1521,9 +1540,11 @@ static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const
     struct G { const uint16_t* a; int ka; const uint16_t* b; int kb; int64_t off, boff; };
     const G gs[3] = {{xT, 64, dh1T, MLP_HID, 0, o_b1}, {h1T, MLP_HID, dh2T, MLP_HID, o_w2, o_b2},
                      {h2T, MLP_HID, gyT, MLP_OUT, o_w3, o_b3}};
-    // one workgroup per CU owns a share of the chunk's rows and the whole
-    // output (pg.hip); the split count is fixed for a given Mpad
-    const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(c->cus, Mpad / 256));
+    // one workgroup per split owns a share of the chunk's rows and the whole
+    // output (pg.hip); the split count is a function of Mpad alone (256 = the
+    // MI355X's CU count, not the device's), so the gradient's summation order
+    // and bits do not depend on the GPU or its partition mode
+    const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(kPgSplits, Mpad / 256));
     // each split's partials in the packed gradient order (w1 | b1 | w2 | b2 |
     // w3 | b3): one reduction for the three GEMMs
     const int64_t need = (int64_t)splits * kGradFloats;

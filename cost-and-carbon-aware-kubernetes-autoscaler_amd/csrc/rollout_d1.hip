@@ -165,9 +165,12 @@ namespace {
 // Opaque copy of a kernel argument: the value then lives in a register for the
 // whole loop (spilled to a VGPR lane if need be) instead of being re-read from
 // the kernarg segment with an s_load + lgkmcnt wait at each use.
+#ifndef D1_OPQ_V
+#define D1_OPQ_V 1
+#endif
 template <class V>
 __device__ __forceinline__ V opq(V v) {
-  asm volatile("" : "+s"(v));
+  if constexpr (D1_OPQ_V) asm volatile("" : "+s"(v));
   return v;
 }
 // global-memory pointer made opaque the same way, keeping its address space
@@ -176,7 +179,7 @@ __device__ __forceinline__ V opq(V v) {
 template <class V>
 __device__ __forceinline__ GLOBAL_AS V* opq_ptr(V* v) {
   uint64_t x = (uint64_t)v;
-  asm volatile("" : "+s"(x));
+  if constexpr (D1_OPQ_V) asm volatile("" : "+s"(x));
   return (GLOBAL_AS V*)x;
 }
 // per-lane variant: the value is redefined by the asm, so no load is pending
@@ -338,6 +341,11 @@ constexpr int D1_NOSTORE = 0x7FFFFFF0;
 // faster than none in round 3, whatever the level and direction (the gain is
 // as much the s_setprio boundaries as the arbitration)
 constexpr int D1_PRIO_HI = 3;
+// quiet steps in parallel-prefix form (1) or one after another (0: the A/B
+// variant, tools/build_variants.py)
+#ifndef D1_PQ_V
+#define D1_PQ_V 0
+#endif
 __device__ __forceinline__ void d1_store_rec(__amdgpu_buffer_rsrc_t r, int voff, const int4& v) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   const i32x4 x = {v.x, v.y, v.z, v.w};
@@ -1910,6 +1918,70 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     D1_STAMP(8);
     // ---- quiet steps: up to D1_S per iteration and lane ----
     const int tlim = min(T, t_rdy);
+    if constexpr (BDEF && D1_PQ_V) {
+      // The LEAN 2 quiet steps in parallel-prefix form (the same decisions as
+      // the sequential form below). A lane that fails a sub-step never steps
+      // again in this iteration (stall is sticky and t stops), so the steps it
+      // takes are a prefix q < n of its D1_S samples and sub-step q runs at
+      // t0 + q. Each sample's test is then independent of the others except
+      // for the down-window hold, which depends only on where the earlier
+      // samples proposed >= cur. The tests are the sign bits of integer
+      // differences combined with VALU bit operations: no per-lane mask
+      // travels through scalar registers and nothing branches, so the D1_S
+      // sub-steps issue as independent vector work instead of a compare ->
+      // scalar mask -> select chain per step. Usages are compared clamped to
+      // [0, 2^21] as unsigned: every step taken has 0 <= usage < q_ulim <=
+      // 2^20, where the clamp is the identity, and a negative usage fails
+      // (uint32) usage < q_ulim as in the sequential test.
+      constexpr int UC = 1 << 21;
+      const int t0 = t;
+      const int hb = t0 - 1 - q_hold;      // sign(hb + q): t0 + q <= q_hold
+      const int dm = t0 - min(nxt, tlim);  // sign(dm + q): t0 + q < nxt and t0 + q < tlim
+      const int cw = -1 - wl;              // sign(cw + q + mg): the last sample before q with
+                                           // proposal >= cur lies within wl steps
+      int P = stall ? 0 : -1;  // sign bit: the lane still steps
+      int mg = 64;             // -(index of the last sample so far with proposal >= cur); 64: none
+      int mp = 64;             // mg as it stood after the lane's last step
+      int nneg = 0, sneg = 0, sat = 0;
+      uint32_t us = 0;
+      const int vb = lb + t0 * 16;
+#pragma unroll
+      for (int q = 0; q < D1_S; ++q) {
+        const int usage = min(Lpf[q], q_rcap);
+        const int uc = (int)min((uint32_t)usage, (uint32_t)UC);
+        const int d_lt = uc - q_ulim;   // sign: usage < q_ulim
+        const int d_nge = uc - q_pge;   // sign: proposal < cur
+        const int d_slo = uc - q_slo;   // sign: no SLO miss
+        const int hold = (hb + q) | (cw + q + mg);
+        P &= d_lt & (dm + q) & (int)bfi((uint32_t)d_nge, (uint32_t)hold, 0xFFFFFFFFu);
+        const int pm = P >> 31;  // -1: the lane takes this step
+        mg = (int)bfi((uint32_t)(d_nge >> 31), (uint32_t)mg, (uint32_t)-q);
+        mp = (int)bfi((uint32_t)pm, (uint32_t)mg, (uint32_t)mp);
+        const int upp = (int)fmaf((float)uc, q_rbp, q_hbp);
+        nneg += pm;
+        us += (uint32_t)(pm & upp);
+        sneg += (pm & ~d_slo) >> 31;
+        sat |= pm & (q_usat - upp);
+        const int w = (int)bfi((uint32_t)(d_slo >> 31), (uint32_t)q_w0, (uint32_t)q_w1);
+        d1_store_rec(trs, (int)bfi((uint32_t)pm, (uint32_t)vb, (uint32_t)D1_NOSTORE) + 16 * q,
+                     make_int4(replicas, q_pendv, q_nodes, w));
+      }
+      const int n = -nneg;
+      if (__builtin_expect(sat < 0, 0)) {  // a step taken may saturate a node: exact per-node sums
+#pragma unroll
+        for (int q = 0; q < D1_S; ++q) {
+          const int uc = (int)min((uint32_t)min(Lpf[q], q_rcap), (uint32_t)UC);
+          const int upp = (int)fmaf((float)uc, q_rbp, q_hbp);
+          if (q < n && upp > q_usat) e_hour += dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
+        }
+      }
+      usum += us;
+      slo -= sneg;
+      stall = stall || n < min(D1_S, tlim - t0);
+      if (mp <= 0) q_hold = max(q_hold, t0 - mp + wl);
+      t = t0 + n;
+      adv = n > 0;
+    } else
 #pragma unroll
     for (int sub = 0; sub < D1_S; ++sub) {
     if constexpr (BDEF) {

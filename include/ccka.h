@@ -273,8 +273,8 @@ typedef struct ccka_traj_rec {
  * ccka_totals_finish), so they too are bit-identical at any rank count.
  * Units and headroom: energy in microwatt-minutes (a config-3 scenario, one
  * day on up to 8 nodes, is ~8.6e9 uW.min, so int64 holds ~1e9 such scenarios
- * summed over all ranks), gCO2 in micrograms (~5.7e10 ug per such scenario at
- * 400 g/kWh: ~1.6e8 scenarios). A sum that would leave int64 is reported as
+ * summed over all ranks), gCO2 in micrograms (~5.7e7 ug per such scenario at
+ * 400 g/kWh: ~1.6e11 scenarios). A sum that would leave int64 is reported as
  * CCKA_EOVERFLOW (ccka_get_totals, ccka_totals_finish,
  * ccka_allreduce_totals), never wrapped. */
 typedef struct ccka_totals {
@@ -461,7 +461,9 @@ typedef struct ccka_mlp_grads {
  * Device memory: the loop's features, 128 B per (step, scenario) row, plus
  * the backward's work arrays for one chunk of at most 2^23 rows (2,192 B per
  * row, ~18 GB); chunks run in order and their gradients add up in that order,
- * so the result depends on N*T only (1e7 x 60 rows: ~80 GB in all). */
+ * so the result depends on N*T only, on any GPU (1e7 x 60 rows: ~78 GB of
+ * features + ~18 GB of work arrays, ~96 GB in all; the single-deployment
+ * kernel's tiled trace copy, N*T*4 B, is released for the loop). */
 int ccka_policy_grad(ccka_ctx* ctx, const ccka_pg_params* params, ccka_mlp_grads* out, double* objective_mean);
 /* The sampled action bins [T][N] and the per-scenario factors (J_i - b) / N of
  * the last ccka_policy_grad (count = T*N). */

@@ -262,7 +262,7 @@ def test_d1_edge_cases(engine, variant):
 
 def test_d1_trace_layouts(engine):
     """The single-deployment kernel reads its wave-tiled trace copy
-    ([wave][T][lanes], built at gen_load / set_load); the [T][N] trace
+    ([wave][T][lanes], built by the first rollout of a trace); the [T][N] trace
     (ccka_debug_trace_flat) and a re-tiling after the lanes-per-wave value
     changes under a resident trace give the same bit-exact results and
     trajectories as the oracle."""

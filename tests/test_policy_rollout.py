@@ -146,3 +146,66 @@ def test_closed_loop_fused_equals_launched(engine, drift):
     at2, ac2 = engine.policy_actions()
     rc = po.rollout_policy(spec, sc2, load, at2, ac2, threads=THREADS)[0]
     compare(engine.results(), rc)
+
+
+def _policy_hooks(engine):
+    import ctypes as C
+    hooks = {}
+    for name in ("ccka_debug_policy_fused", "ccka_debug_policy_table", "ccka_debug_policy_graph"):
+        fn = getattr(engine.lib, name)
+        fn.argtypes = [C.c_void_p, C.c_int32]
+        hooks[name.rsplit("_", 1)[1]] = fn
+    return hooks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["pool_limit", "no_table"])
+@pytest.mark.parametrize("pol", [1, 2])
+def test_fused_loop_catalog_scans_equal_launched(engine, variant, pol):
+    """The fused loop on its catalog-scan path (no argmin tables: a world with
+    NodePool CPU limits, which d1_check_world refuses, or the tables turned
+    off with ccka_debug_policy_table(0)) against the launched loop, for the
+    deterministic policy (POL 1) and the sampled one of the policy gradient
+    (POL 2): results, trajectories, actions / sampled bins, every step's
+    features and, for POL 2, the gradient are bit-identical; POL 1 also equals
+    the oracle's replay of its actions."""
+    spec, sc, load = _case(n=384, T=120)
+    if variant == "pool_limit":
+        for p in spec.pools:
+            p.limit_cpu_m = 6000
+    ws, bs = configs.mlp_weights(11)
+    engine.set_world(spec)
+    engine.set_scenarios(sc)
+    engine.set_load(load)
+    engine.mlp_set_weights([configs.to_bf16_bits(w) for w in ws], bs)
+    h = _policy_hooks(engine)
+    runs = []
+    engine.debug_policy_features(True)
+    try:
+        h["table"](engine.ctx, 0 if variant == "no_table" else 1)
+        for fused in (1, 0):
+            h["fused"](engine.ctx, fused)
+            if pol == 1:
+                engine.policy_rollout(trajectory=True, record=True)
+                extra = engine.policy_actions()
+                tr = engine.trajectory()
+            else:
+                g, obj = engine.policy_grad(seed=3, w_carbon=0.05, w_slo=0.01)
+                extra = engine.policy_samples() + (obj,)
+                extra = extra + tuple(np.array(g[k]) for k in sorted(g))
+                tr = None
+            assert engine.last_engine()[0] == (4 if fused else 3)
+            runs.append((engine.results(), tr, extra, engine.debug_get_policy_features()))
+    finally:
+        h["fused"](engine.ctx, 1)
+        h["table"](engine.ctx, 1)
+        engine.debug_policy_features(False)
+    (r0, t0, x0, f0), (r1, t1, x1, f1) = runs
+    compare(r1, r0, t1, t0)
+    assert all(np.array_equal(a, b) for a, b in zip(x0, x1))
+    assert np.array_equal(f0, f1)
+    if pol == 1:
+        at, ac = x0
+        assert at.std() > 0
+        rc, tc = po.rollout_policy(spec, sc, load, at, ac, traj=True, threads=THREADS)
+        compare(r0, rc, t0, tc)

@@ -20,4 +20,9 @@ fi
 [ -f $src/c5p7/run_kernel_stats.csv ] && cp $src/c5p7/run_kernel_stats.csv "$dst/config5_policy_1e7_kernel_stats.csv"
 [ -f $src/c5g/run_kernel_stats.csv ] && cp $src/c5g/run_kernel_stats.csv "$dst/config5_grad_kernel_stats.csv"
 [ -f $src/loop_split_1e7.txt ] && cp $src/loop_split_1e7.txt "$dst/"
+# the tree the profiles were taken from (bench.py labels the fields it copies from them)
+head=$(git rev-parse --short=12 HEAD)$(git diff --quiet -- cost-and-carbon-aware-kubernetes-autoscaler_amd/csrc || echo "+dirty")
+for f in "$dst/config2_traj_summary.json" "$dst/issue_config234.json"; do
+  [ -f "$f" ] && python3 -c "import json,sys; p=sys.argv[1]; d=json.load(open(p)); d['source_head']=sys.argv[2]; json.dump(d,open(p,'w'),indent=1)" "$f" "$head"
+done
 ls "$dst"
