@@ -348,7 +348,7 @@ def main():
                        + (f", disruption budget {args.budget} %" if args.budget is not None else ""),
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
-                       "trace_layout": "[T][N] (shared traces)" if cfg == 4 else "[T][N]" if args.trace_flat else "wave-tiled [wave][T][lanes] (built at gen_load)",
+                       "trace_layout": "[T][N] (shared traces)" if cfg == 4 else "[T][N]" if args.trace_flat else "wave-tiled [wave][T][lanes] (built by the first rollout)",
                        "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

@@ -289,7 +289,14 @@ static int d1_check_world(ccka_ctx* c) {
   c->d1_world = false;
   c->d1_ready = false;
   const ccka_deployment& dp = w.deploy[0];
-  if (w.n_deploy != 1 || dp.scaler != CCKA_SCALER_HPA) return CCKA_OK;
+  // one HPA deployment, or one single-trigger KEDA ScaledObject (default
+  // behavior, one decision per step: the KEDA instantiation)
+  const bool keda = dp.scaler == CCKA_SCALER_KEDA;
+  if (w.n_deploy != 1 || (dp.scaler != CCKA_SCALER_HPA && !keda)) return CCKA_OK;
+  if (keda && (w.hpa_sync_s == 15 || w.max_nodes > 8 || w.n_pools > 2 || dp.keda_threshold < 1 || dp.keda_threshold >= (1 << 22) ||
+               dp.keda_activation < INT32_MIN || dp.keda_activation >= INT32_MAX || dp.keda_min < 0 ||
+               dp.keda_min > D1_REC_SAT || dp.keda_max < 0 || dp.keda_max > D1_REC_SAT))
+    return CCKA_OK;
   // pool limits run on the general kernel; drift, replacement and multi-node
   // consolidation are checked per scenario set in d1_prepare (d1_disrupt_ok)
   for (int q = 0; q < w.n_pools; ++q)
@@ -380,6 +387,15 @@ static int d1_check_world(ccka_ctx* c) {
   p.bdef = d1_rule_is_default(p.up, true) && d1_rule_is_default(p.dn, false);
   p.nsub = sync15 ? 4 : 1;
   if (sync15 && (!p.bdef || dp.down.stab_window_s > kD1Sync15MaxWindow)) return CCKA_OK;
+  if (keda) {
+    if (!p.bdef || dp.down.stab_window_s > CCKA_HIST * CCKA_STEP_SECONDS) return CCKA_OK;
+    p.keda = 1;
+    p.k_thr = (int32_t)dp.keda_threshold;
+    p.k_act = (int32_t)dp.keda_activation;
+    p.k_cds = dp.keda_cooldown_s > 0 ? (int32_t)std::min<int64_t>(((int64_t)dp.keda_cooldown_s + 59) / 60, 1 << 20) : 0;
+    p.k_min = dp.keda_min;
+    p.k_max = dp.keda_max;
+  }
   c->d1_world = true;
   return CCKA_OK;
 }
@@ -462,15 +478,20 @@ static int d1_prepare(ccka_ctx* c) {
   c->d1_ready = true;
   c->d1_ok = false;
   bool drift = false, replace = false, multi = false;
-  if (!c->d1_world || !c->sc_maxr_ok || !d1_disrupt_ok(c, &drift, &replace, &multi)) return CCKA_OK;
+  // (a KEDA deployment ignores the per-scenario target / max / down-window
+  // overrides: its bounds and rules are the ScaledObject's, SEMANTICS 3.C)
+  const bool keda = c->d1.keda != 0;
+  if (!c->d1_world || (!keda && !c->sc_maxr_ok) || !d1_disrupt_ok(c, &drift, &replace, &multi)) return CCKA_OK;
+  if (keda && (drift || replace || multi)) return CCKA_OK;  // the KEDA instantiation has no DRIFT paths
   c->d1.drift = (drift || replace || multi) ? 1 : 0;  // the DRIFT instantiation carries all three
   c->d1.drift_on = drift ? 1 : 0;
   c->d1.replace = replace ? 1 : 0;
   c->d1.multi = multi ? 1 : 0;
   // beyond the register ring
-  if (c->sc_dstab_max > (c->d1.nsub == 4 ? kD1Sync15MaxWindow : CCKA_HIST * CCKA_STEP_SECONDS)) return CCKA_OK;
+  if (!keda && c->sc_dstab_max > (c->d1.nsub == 4 ? kD1Sync15MaxWindow : CCKA_HIST * CCKA_STEP_SECONDS))
+    return CCKA_OK;
   // default behavior and no window beyond 300 s: the 4-record ring instantiation
-  c->d1.he4 = (c->d1.nsub == 1 && c->d1.bdef && c->d1.dstab0 <= 300 && c->sc_dstab_max <= 300) ? 1 : 0;
+  c->d1.he4 = (c->d1.nsub == 1 && c->d1.bdef && c->d1.dstab0 <= 300 && (keda || c->sc_dstab_max <= 300)) ? 1 : 0;
   const size_t n = (size_t)c->N;
   std::vector<double> wl;
   std::vector<uint8_t> wci;

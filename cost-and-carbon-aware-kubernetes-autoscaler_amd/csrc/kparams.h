@@ -245,6 +245,14 @@ struct D1Params {
   int32_t nsub;                      // HPA decisions per step: 1, or 4 (15 s sync, default behavior)
   int32_t he4;                       // every down window <= 300 s (a 4-record ring suffices)
   int32_t multi;                     // 1: multi-node consolidation (SEMANTICS 3.G3) acts (DRIFT instantiation)
+  // KEDA ScaledObject deployment (SEMANTICS 3.C, one trigger; the KEDA
+  // instantiation: default behavior, one decision per step, no drift)
+  int32_t keda;
+  int32_t k_thr;   // AverageValue threshold per replica, 1 .. 2^22 - 1
+  int32_t k_act;   // activationThreshold (int32; < INT32_MAX)
+  int32_t k_cds;   // cooldownPeriod in whole steps: ceil(cooldown_s / 60), >= 0
+  int32_t k_min;   // minReplicaCount
+  int32_t k_max;   // maxReplicaCount
 };
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)

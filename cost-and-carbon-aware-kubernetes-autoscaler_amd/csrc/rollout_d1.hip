@@ -165,12 +165,9 @@ namespace {
 // Opaque copy of a kernel argument: the value then lives in a register for the
 // whole loop (spilled to a VGPR lane if need be) instead of being re-read from
 // the kernarg segment with an s_load + lgkmcnt wait at each use.
-#ifndef D1_OPQ_V
-#define D1_OPQ_V 1
-#endif
 template <class V>
 __device__ __forceinline__ V opq(V v) {
-  if constexpr (D1_OPQ_V) asm volatile("" : "+s"(v));
+  asm volatile("" : "+s"(v));
   return v;
 }
 // global-memory pointer made opaque the same way, keeping its address space
@@ -179,7 +176,7 @@ __device__ __forceinline__ V opq(V v) {
 template <class V>
 __device__ __forceinline__ GLOBAL_AS V* opq_ptr(V* v) {
   uint64_t x = (uint64_t)v;
-  if constexpr (D1_OPQ_V) asm volatile("" : "+s"(x));
+  asm volatile("" : "+s"(x));
   return (GLOBAL_AS V*)x;
 }
 // per-lane variant: the value is redefined by the asm, so no load is pending
@@ -341,11 +338,6 @@ constexpr int D1_NOSTORE = 0x7FFFFFF0;
 // faster than none in round 3, whatever the level and direction (the gain is
 // as much the s_setprio boundaries as the arbitration)
 constexpr int D1_PRIO_HI = 3;
-// quiet steps in parallel-prefix form (1) or one after another (0: the A/B
-// variant, tools/build_variants.py)
-#ifndef D1_PQ_V
-#define D1_PQ_V 0
-#endif
 __device__ __forceinline__ void d1_store_rec(__amdgpu_buffer_rsrc_t r, int voff, const int4& v) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   const i32x4 x = {v.x, v.y, v.z, v.w};
@@ -417,10 +409,15 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
 // loops; launch_rollout_d1 picks it from the scenarios' largest window)
 // G3: the DRIFT instantiation with multi-node consolidation (budgets of >= 2
 // nodes; its trial copies of the slots would spill in the others)
+// KEDA: the deployment is a single-trigger KEDA ScaledObject (SEMANTICS 3.C:
+// activation, scale from / to zero after the cooldown, proposal
+// ceil(metric / threshold) outside the tolerance band of the current count)
+// with the default behavior, one decision per step
 template <int MAXN, int MAXP, bool STAMPS, int OCC, bool BDEF, bool DRIFT = false, int NSUB = 1, int HE = 8,
-          bool G3 = false>
+          bool G3 = false, bool KEDA = false>
 __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   static_assert(NSUB == 1 || (NSUB == 4 && BDEF), "15 s sync: lean default path");
+  static_assert(!KEDA || (BDEF && NSUB == 1 && !DRIFT), "KEDA: default behavior, one decision per step");
   static_assert(HE == 8 || (HE == 4 && NSUB == 1 && BDEF), "4-record ring: default behavior, one decision per step");
   static_assert(!G3 || (DRIFT && MAXP == 2), "G3: the DRIFT instantiation, two pools");
   constexpr int HW = NSUB == 1 ? HE / 2 : 10;  // history words (2 records each)
@@ -462,9 +459,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 
   // ---- per-scenario parameters ----
   const int r = p.region ? (int)p.region[i] : 0;
-  const int target = p.target ? (int)p.target[i] : p.target0;
-  const int mx = p.maxr ? (int)p.maxr[i] : p.maxr0;
-  const int dwin = p.down_stab ? (int)p.down_stab[i] : p.dstab0;
+  // (a KEDA ScaledObject has no utilisation target, and its replica bounds and
+  // down window are its own: the scenario's target / max / window overrides
+  // are the HPA's)
+  const int target = KEDA ? 1 : (p.target ? (int)p.target[i] : p.target0);
+  const int mx = KEDA ? opq(p.k_max) : (p.maxr ? (int)p.maxr[i] : p.maxr0);
+  const int dwin = (!KEDA && p.down_stab) ? (int)p.down_stab[i] : p.dstab0;
   // records inside the down window: entries k < (W - 1) / sync (o_entries)
   const int nd = min(NSUB == 1 ? __popc(wmask(dwin)) : (dwin > 15 ? (dwin - 1) / 15 : 0), 2 * HW);
   const int dnmask = NSUB == 1 ? wmask(dwin) : 0;
@@ -472,7 +472,12 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   const int pswitch = p.pswitch ? (int)p.pswitch[i] : p.pswitch0;
   const int wi = p.wci ? (int)p.wci[i] : 0;
   const uint32_t capsel = p.cap_sel ? (uint32_t)p.cap_sel[i] : (uint32_t)p.capsel0;
-  const int minr = opq(p.minr), req = opq(p.req_cpu), limit = opq(p.limit);
+  // KEDA: the HPA path's minimum is max(minReplicaCount, 1) (0 only by the cooldown)
+  const int minr = KEDA ? max(opq(p.k_min), 1) : opq(p.minr), req = opq(p.req_cpu), limit = opq(p.limit);
+  // KEDA trigger: threshold per replica, activation, cooldown in steps
+  const int kthr = KEDA ? opq(p.k_thr) : 1, kact = KEDA ? opq(p.k_act) : 0, kcds = KEDA ? opq(p.k_cds) : 0;
+  const bool kmin0 = KEDA && opq(p.k_min) == 0;
+  const float rkthr = __builtin_amdgcn_rcpf((float)kthr);
   // 1-tol <= fl(util/target) <= 1+tol  <=>  ulo <= util <= uhi (fl(u/t) is monotone in u)
   int ulo = max(0, (int)floor(p.tol_lo * (double)target) - 2);
   while ((double)ulo / (double)target < p.tol_lo) ++ulo;
@@ -615,6 +620,27 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     dn16[w] = (2 * w < nd ? 0xFFFFu : 0u) | (2 * w + 1 < nd ? 0xFFFF0000u : 0u);
   }
   int next_ready = 0x7fffffff, nsp = 0, nod = 0;
+  // KEDA: the cooldown runs out at kcd (the last active step + the cooldown;
+  // last_active = 0 initially); the current replica count's tolerance band of
+  // the metric: proposal = cur exactly on [q_klo, q_khi]
+  int kcd = kcds, q_klo = 0, q_khi = -1, kb_cur = -1;
+  bool q_kcd = false;  // the quiet steps must check the cooldown (replicas > 0, minReplicaCount 0)
+  bool k_act_step = false;  // the step's trigger activity (the SLO reads it)
+  // within(r), r = double(L) / (double(threshold) * double(cur)), is monotone
+  // in L: the band's ends by the binary64 test itself around an estimate
+  auto keda_band = [&](int cur) {
+    if (!KEDA || cur == kb_cur) return;
+    kb_cur = cur;
+    if (cur <= 0) { q_klo = 0; q_khi = -1; return; }
+    const double D = (double)kthr * (double)cur;
+    long long lo = max((long long)floor(p.tol_lo * D) - 2, -1LL);
+    while ((double)lo / D < p.tol_lo) ++lo;
+    long long hi = (long long)floor(p.tol_hi * D) + 2;
+    while ((double)hi / D > p.tol_hi) --hi;
+    q_klo = (int)min(lo, 0x7fffffffLL);
+    q_khi = (int)min(hi, 0x7ffffffeLL);
+  };
+  keda_band(p.replicas0);
   // free pod capacity of the compatible ready slots (kept incrementally)
   int Ffree = 0;
   // smallest pod capacity of any node launched so far (refreshed on deletion):
@@ -683,6 +709,40 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     int util, proposal, desired;
     bool ran, hpa_path;
   };
+  // steps 4-5 for a decision that produced a proposal: the stabilisation
+  // (packed min / max over the records inside each window), the rate limits
+  // and the [minr, mx] clamp
+  auto behave = [&](int proposal, int cur) -> int {
+    int upr = proposal, dnr = proposal;
+    if (rup.stab_mask) {  // wave-uniform
+      short2v a = as_s2(bfi((uint32_t)rup.stab16[0], hup[0], 0x7FFF7FFFu));
+#pragma unroll
+      for (int w = 1; w < 4; ++w)
+        a = __builtin_elementwise_min(a, as_s2(bfi((uint32_t)rup.stab16[w], hup[w], 0x7FFF7FFFu)));
+      upr = min(upr, min((int)a.x, (int)a.y));
+    }
+    {
+      short2v a = as_s2(bfi(dn16[0], hdn[0], 0x80008000u));
+#pragma unroll
+      for (int w = 1; w < HW; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
+      dnr = max(dnr, max((int)a.x, (int)a.y));
+    }
+    const int rc = min(max(cur, upr), dnr);
+    int lo = minr, hi = mx;
+    if constexpr (BDEF) {
+      // up: max(Percent 100 -> ceil(2.0*cur), Pods 4 -> cur+4) over 15 s
+      // periods (no 60 s history inside), never below cur; down: Percent 100
+      // -> int(cur*0.0) = 0, never above cur
+      hi = rc > cur ? min(hi, max(2 * cur, cur + 4)) : hi;
+      lo = rc < cur ? max(lo, 0) : lo;
+    } else {
+      if (proposal != cur) {
+        if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
+        else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+      }
+    }
+    return rc < lo ? lo : (rc > hi ? hi : rc);
+  };
   auto hpa_eval = [&](int L, int cur, int ready, float rbd, float rbc) -> HpaOut {
     HpaOut o;
     const bool metric = cur <= mx && cur >= minr && ready > 0 && !(cur == 0 && minr != 0);
@@ -720,37 +780,47 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     o.ran = metric;
     o.hpa_path = !(cur == 0 && minr != 0);
     int desired = cur > mx ? mx : (cur < minr && o.hpa_path ? minr : cur);
-    {
-      int upr = proposal, dnr = proposal;
-      if (rup.stab_mask) {  // wave-uniform
-        short2v a = as_s2(bfi((uint32_t)rup.stab16[0], hup[0], 0x7FFF7FFFu));
-#pragma unroll
-        for (int w = 1; w < 4; ++w)
-          a = __builtin_elementwise_min(a, as_s2(bfi((uint32_t)rup.stab16[w], hup[w], 0x7FFF7FFFu)));
-        upr = min(upr, min((int)a.x, (int)a.y));
-      }
-      {
-        short2v a = as_s2(bfi(dn16[0], hdn[0], 0x80008000u));
-#pragma unroll
-        for (int w = 1; w < HW; ++w) a = __builtin_elementwise_max(a, as_s2(bfi(dn16[w], hdn[w], 0x80008000u)));
-        dnr = max(dnr, max((int)a.x, (int)a.y));
-      }
-      const int rc = min(max(cur, upr), dnr);
-      int lo = minr, hi = mx;
-      if constexpr (BDEF) {
-        // up: max(Percent 100 -> ceil(2.0*cur), Pods 4 -> cur+4) over 15 s
-        // periods (no 60 s history inside), never below cur; down: Percent 100
-        // -> int(cur*0.0) = 0, never above cur
-        hi = rc > cur ? min(hi, max(2 * cur, cur + 4)) : hi;
-        lo = rc < cur ? max(lo, 0) : lo;
+    if (metric && !(ablate & 8)) desired = behave(proposal, cur);
+    o.desired = desired;
+    return o;
+  };
+  // KEDA (SEMANTICS 3.C): activity, scale from / to zero, then the HPA steps
+  // 1, 4, 5, 6 on the proposal ceil(L / threshold) outside the band
+  auto keda_eval = [&](int L, int cur, int ts) -> HpaOut {
+    HpaOut o{};
+    const bool act = L > kact;
+    const bool cool = !act && kmin0 && ts >= kcd;
+    if (act) kcd = ts + kcds;
+    k_act_step = act;
+    o.util = 0;
+    o.proposal = cur;
+    o.ran = false;
+    o.hpa_path = false;
+    int desired = cur;
+    if (cur == 0) {
+      desired = act ? 1 : 0;
+    } else if (cool) {
+      desired = 0;
+    } else {
+      o.hpa_path = true;
+      if (cur > mx) {
+        desired = mx;
+      } else if (cur < minr) {
+        desired = minr;
       } else {
-        if (metric && proposal != cur) {
-          if (rc > cur) hi = min(hi, max(rate_limit1(rup, true, cur, hdel), cur));
-          else if (rc < cur) lo = max(lo, min(rate_limit1(rdn, false, cur, hdel), cur));
+        int prop = cur;
+        if (L < q_klo || L > q_khi) {
+          // int32(ceil(double(L) / double(threshold))) is the exact integer
+          // ceiling for 0 <= L and threshold < 2^22 (d1_check_world)
+          bool slow = L < 0;
+          const int q = fdiv_nb(max(L, 0), kthr, rkthr, slow);
+          prop = q + (q * kthr != L ? 1 : 0);
+          if (__builtin_expect(slow, 0)) prop = (int)ceil((double)L / (double)kthr);
         }
+        o.proposal = prop;
+        o.ran = true;
+        desired = (ablate & 8) ? cur : behave(prop, cur);
       }
-      const int db = rc < lo ? lo : (rc > hi ? hi : rc);
-      if (metric && !(ablate & 8)) desired = db;
     }
     o.desired = desired;
     return o;
@@ -920,11 +990,21 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             bool anylow = false;
 #pragma unroll
             for (int j = 0; j < JR; ++j) {
-              us[j] = min(ring[ridx(rnext(tr, rbn - 1 - j))], q_rcap);
+              us[j] = KEDA ? ring[ridx(rnext(tr, rbn - 1 - j))] : min(ring[ridx(rnext(tr, rbn - 1 - j))], q_rcap);
               rv[j] = q_met ? cur16 : (int)0x8000;
               anylow |= (j < kq) & q_met & (us[j] < q_pge);
             }
-            if (anylow) {
+            if (KEDA && anylow) {
+              // held below cur (KEDA): the proposal ceil(L / threshold) < cur,
+              // an exact integer ceiling (0 <= L < 2^20)
+#pragma unroll
+              for (int j = 0; j < JR; ++j) {
+                bool sl = false;
+                const bool low = (j < kq) & q_met & (us[j] < q_pge);
+                const int q = fdiv_nb(max(us[j], 0), kthr, rkthr, sl);
+                rv[j] = low ? min(q + (q * kthr != us[j] ? 1 : 0), D1_REC_SAT) : rv[j];
+              }
+            } else if (anylow) {
               // held below cur: util < ulo <= target, so no unready rule and the
               // proposal is ceil(util * ready / target) (binary64 at an exact
               // multiple, as the spec writes it); us < 2^20 and util < 2^15 keep
@@ -1053,8 +1133,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 #pragma unroll
         for (int sub = 0; sub < NSUB; ++sub) {
           const int cur = replicas;
-          hp = hpa_eval(L, cur, rpods, __builtin_amdgcn_rcpf((float)(rpods * req)),
-                        __builtin_amdgcn_rcpf((float)(cur * req)));
+          if constexpr (KEDA) hp = keda_eval(L, cur, t);
+          else
+            hp = hpa_eval(L, cur, rpods, __builtin_amdgcn_rcpf((float)(rpods * req)),
+                          __builtin_amdgcn_rcpf((float)(cur * req)));
           hpa_commit(hp, cur);
           replicas = hp.desired;
         }
@@ -1768,7 +1850,10 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         cost += burn + base_price;
         e_hour += e_step;
         const int pending = replicas - rpods;
-        if (pending > 0 || (hp.ran && hp.util > slo_util)) { slo++; flags |= 8u; }
+        // SLO: pending pods, an HPA's utilisation above the threshold, or an
+        // active KEDA trigger with no replica
+        const bool slo_s = KEDA ? (k_act_step && replicas == 0) : (hp.ran && hp.util > slo_util);
+        if (pending > 0 || slo_s) { slo++; flags |= 8u; }
         pend_min += pending;
         nmin_spot += nsp;
         nmin_od += nod;
@@ -1786,7 +1871,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             return a > 100ull * UQ ? UQ : min((int)(((uint32_t)a + 99u) / 100u), UQ);
           };
           const bool hpa_path = !(replicas == 0 && minr != 0);
-          const bool met = replicas <= mx && replicas >= minr && rpods > 0 && hpa_path;
+          bool met = replicas <= mx && replicas >= minr && rpods > 0 && hpa_path;
           const int dnm = replicas > mx ? mx : (replicas < minr && hpa_path ? minr : replicas);
           const bool pend = replicas > rpods;
           q_met = met;
@@ -1825,6 +1910,31 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
             if (!pend) slo_thr = umin(max(slo_util + 1, 0), dreq);
           } else if (dnm == replicas) {
             ulim = UQ;  // no metric, replicas in range: every step keeps them
+          }
+          if constexpr (KEDA) {
+            // the ScaledObject's metric: quiet while the decision keeps the count
+            // (replicas 0: while the trigger is inactive; in [minr, mx]: below
+            // the band's top (any metric at mx), with proposal >= cur, i.e. in
+            // the band or ceil(L / threshold) >= cur, from min(q_klo,
+            // (cur - 1) * threshold + 1) on, or held by a record >= cur; the
+            // cooldown is checked per step), no SLO miss but pending pods
+            met = false;
+            ulim = 0;
+            pge = UQ;
+            slo_thr = pend ? 0 : UQ;
+            q_kcd = false;
+            if (replicas == 0) {
+              ulim = (int)min(max((long long)kact + 1, 0LL), (long long)UQ);
+              pge = 0;
+            } else if (replicas >= minr && replicas <= mx) {
+              met = true;
+              q_kcd = kmin0;
+              keda_band(replicas);
+              ulim = replicas >= mx ? UQ : (int)min((long long)q_khi + 1, (long long)UQ);
+              const long long lc = (long long)(replicas - 1) * kthr + 1;
+              pge = (int)max(0LL, min(min((long long)q_klo, lc), (long long)UQ));
+            }
+            q_met = met;
           }
           q_ulim = ulim;
           q_pge = pge;
@@ -1918,84 +2028,25 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     D1_STAMP(8);
     // ---- quiet steps: up to D1_S per iteration and lane ----
     const int tlim = min(T, t_rdy);
-    if constexpr (BDEF && D1_PQ_V) {
-      // The LEAN 2 quiet steps in parallel-prefix form (the same decisions as
-      // the sequential form below). A lane that fails a sub-step never steps
-      // again in this iteration (stall is sticky and t stops), so the steps it
-      // takes are a prefix q < n of its D1_S samples and sub-step q runs at
-      // t0 + q. Each sample's test is then independent of the others except
-      // for the down-window hold, which depends only on where the earlier
-      // samples proposed >= cur. The tests are the sign bits of integer
-      // differences combined with VALU bit operations: no per-lane mask
-      // travels through scalar registers and nothing branches, so the D1_S
-      // sub-steps issue as independent vector work instead of a compare ->
-      // scalar mask -> select chain per step. Usages are compared clamped to
-      // [0, 2^21] as unsigned: every step taken has 0 <= usage < q_ulim <=
-      // 2^20, where the clamp is the identity, and a negative usage fails
-      // (uint32) usage < q_ulim as in the sequential test.
-      constexpr int UC = 1 << 21;
-      const int t0 = t;
-      const int hb = t0 - 1 - q_hold;      // sign(hb + q): t0 + q <= q_hold
-      const int dm = t0 - min(nxt, tlim);  // sign(dm + q): t0 + q < nxt and t0 + q < tlim
-      const int cw = -1 - wl;              // sign(cw + q + mg): the last sample before q with
-                                           // proposal >= cur lies within wl steps
-      int P = stall ? 0 : -1;  // sign bit: the lane still steps
-      int mg = 64;             // -(index of the last sample so far with proposal >= cur); 64: none
-      int mp = 64;             // mg as it stood after the lane's last step
-      int nneg = 0, sneg = 0, sat = 0;
-      uint32_t us = 0;
-      const int vb = lb + t0 * 16;
-#pragma unroll
-      for (int q = 0; q < D1_S; ++q) {
-        const int usage = min(Lpf[q], q_rcap);
-        const int uc = (int)min((uint32_t)usage, (uint32_t)UC);
-        const int d_lt = uc - q_ulim;   // sign: usage < q_ulim
-        const int d_nge = uc - q_pge;   // sign: proposal < cur
-        const int d_slo = uc - q_slo;   // sign: no SLO miss
-        const int hold = (hb + q) | (cw + q + mg);
-        P &= d_lt & (dm + q) & (int)bfi((uint32_t)d_nge, (uint32_t)hold, 0xFFFFFFFFu);
-        const int pm = P >> 31;  // -1: the lane takes this step
-        mg = (int)bfi((uint32_t)(d_nge >> 31), (uint32_t)mg, (uint32_t)-q);
-        mp = (int)bfi((uint32_t)pm, (uint32_t)mg, (uint32_t)mp);
-        const int upp = (int)fmaf((float)uc, q_rbp, q_hbp);
-        nneg += pm;
-        us += (uint32_t)(pm & upp);
-        sneg += (pm & ~d_slo) >> 31;
-        sat |= pm & (q_usat - upp);
-        const int w = (int)bfi((uint32_t)(d_slo >> 31), (uint32_t)q_w0, (uint32_t)q_w1);
-        d1_store_rec(trs, (int)bfi((uint32_t)pm, (uint32_t)vb, (uint32_t)D1_NOSTORE) + 16 * q,
-                     make_int4(replicas, q_pendv, q_nodes, w));
-      }
-      const int n = -nneg;
-      if (__builtin_expect(sat < 0, 0)) {  // a step taken may saturate a node: exact per-node sums
-#pragma unroll
-        for (int q = 0; q < D1_S; ++q) {
-          const int uc = (int)min((uint32_t)min(Lpf[q], q_rcap), (uint32_t)UC);
-          const int upp = (int)fmaf((float)uc, q_rbp, q_hbp);
-          if (q < n && upp > q_usat) e_hour += dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
-        }
-      }
-      usum += us;
-      slo -= sneg;
-      stall = stall || n < min(D1_S, tlim - t0);
-      if (mp <= 0) q_hold = max(q_hold, t0 - mp + wl);
-      t = t0 + n;
-      adv = n > 0;
-    } else
 #pragma unroll
     for (int sub = 0; sub < D1_S; ++sub) {
     if constexpr (BDEF) {
         const int L = Lpf[sub];
         // two usage compares decide the HPA (see q_ulim / q_pge); the rest is
         // accounting, the SLO test and the trajectory record, all predicated
-        // on `go` (no branch but the rare saturation one)
+        // on `go` (no branch but the rare saturation one). KEDA compares the
+        // raw metric and checks the cooldown (an active step restarts it).
         const int usage = min(L, q_rcap);
-        const bool ge = usage >= q_pge;
-        const bool ok = (t < nxt) & ((uint32_t)usage < (uint32_t)q_ulim) & (ge | (t <= q_hold));
+        const int cv = KEDA ? L : usage;
+        const bool ge = cv >= q_pge;
+        bool ok = (t < nxt) & ((uint32_t)cv < (uint32_t)q_ulim) & (ge | (t <= q_hold));
+        const bool kac = KEDA && L > kact;
+        if constexpr (KEDA) ok = ok & (!q_kcd | kac | (t < kcd));
         const bool can = !stall & (t < tlim);
         const bool go = ok & can;
         stall = stall | (can & !ok);
         q_hold = (go & ge) ? max(q_hold, t + wl) : q_hold;
+        if constexpr (KEDA) kcd = (go & kac) ? t + kcds : kcd;
         const int upp = (int)fmaf((float)usage, q_rbp, q_hbp);
         if (__builtin_expect(go & (upp > q_usat), 0)) {  // a node may saturate: exact per-node sum instead
           const long long corr = dyn_energy(upp) - (long long)(Ssum * (unsigned long long)(uint32_t)upp);
@@ -2147,7 +2198,10 @@ hipError_t launch_rollout_d1(const D1Params& p, hipStream_t s) {
   }
   // OCC = resident waves per SIMD the register allocation targets
   const bool d = p.bdef != 0;
-  if (p.nsub == 4) {  // 15 s HPA sync, default behavior (d1_check_world)
+  if (p.keda) {  // a KEDA ScaledObject: default behavior, one decision per step, no drift (d1_prepare)
+    if (p.he4) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, false, 1, 4, false, true>), dim3(grid), dim3(B), lds, s, q);
+    else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, false, 1, 8, false, true>), dim3(grid), dim3(B), lds, s, q);
+  } else if (p.nsub == 4) {  // 15 s HPA sync, default behavior (d1_check_world)
     if (p.multi) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 4, 8, true>), dim3(grid), dim3(B), lds, s, q);
     else if (p.drift) hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, true, 4>), dim3(grid), dim3(B), lds, s, q);
     else hipLaunchKernelGGL((rollout_d1_kernel<8, 2, false, 2, true, false, 4>), dim3(grid), dim3(B), lds, s, q);

@@ -207,5 +207,5 @@ def test_fused_loop_catalog_scans_equal_launched(engine, variant, pol):
     if pol == 1:
         at, ac = x0
         assert at.std() > 0
-        rc, tc = po.rollout_policy(spec, sc, load, at, ac, traj=True, threads=THREADS)
-        compare(r0, rc, t0, tc)
+        ref = po.rollout_policy(spec, sc, load, at, ac, traj=True, threads=THREADS)
+        compare(r0, ref[0], t0, ref[1])
