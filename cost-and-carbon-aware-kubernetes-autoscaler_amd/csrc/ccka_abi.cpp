@@ -123,6 +123,11 @@ struct ccka_ctx {
   mlp_bf16x8* d_w1f = nullptr;
   mlp_bf16x8* d_w2f = nullptr;
   mlp_bf16x8* d_w3f = nullptr;
+  // the standalone forward's fragments for v_mfma_f32_16x16x32_bf16 (mlp16_kernel)
+  mlp_bf16x8* d_w1g = nullptr;
+  mlp_bf16x8* d_w2g = nullptr;
+  mlp_bf16x8* d_w3g = nullptr;
+  int mlp_tile = 16;         // standalone forward: 16 (mlp16_kernel) or 32 (mlp_kernel; ccka_debug_mlp_tile)
   float* d_mb = nullptr;  // b1[256] b2[256] b3[8]
   uint16_t* d_mx = nullptr;
   float* d_my = nullptr;
@@ -619,6 +624,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_pol_state); dfree(c->d_pol_target); dfree(c->d_pol_cw); dfree(c->d_rec_target); dfree(c->d_rec_cw);
   dfree(c->d_feat_rec);
   dfree(c->d_w1f); dfree(c->d_w2f); dfree(c->d_w3f); dfree(c->d_mb); dfree(c->d_mx); dfree(c->d_my);
+  dfree(c->d_w1g); dfree(c->d_w2g); dfree(c->d_w3g);
   dfree(c->d_w2b); dfree(c->d_w3b); dfree(c->d_pg_act); dfree(c->d_pg_coef); dfree(c->d_pg_seed); dfree(c->d_pg_x);
   dfree(c->d_pg_work); dfree(c->d_pg_part); dfree(c->d_pg_grad);
   free_results(c);
@@ -2042,6 +2048,10 @@ int ccka_pareto_frontier(ccka_ctx* c, int64_t grid_size, ccka_grid_stats* out, i
 // Layers 2/3 A operand, k-step kk, in the k order of the chained accumulator:
 // element j <-> input unit 32(kk>>1) + 16(kk&1) + 8(j>>2) + 4h + (j&3).
 static int kin(int kk, int j, int h) { return 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3); }
+// 16x16x32 (mlp16_kernel), lane l: i = l & 15 (output row of the tile), g = l >> 4.
+// Layer 1 A operand (natural k): element e = W1[32s + 8g + e][16o + i].
+// Layers 2/3, k-step s, chained order: element e <-> input unit 32s + 16(e>>2) + 4g + (e&3).
+static int kin16(int s, int e, int g) { return 32 * s + 16 * (e >> 2) + 4 * g + (e & 3); }
 
 int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t out_dim, const uint16_t* w1,
                          const float* b1, const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3) {
@@ -2086,6 +2096,27 @@ int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t ou
         const int r = l & 31, h = l >> 5;
         if (h == 0) f3b[((size_t)n * 64 + l) * 8 + j] = w3[(size_t)(32 * n + r) * MLP_OUT + j];
       }
+  std::vector<uint16_t> g1((size_t)16 * 2 * 64 * 8), g2((size_t)16 * 8 * 64 * 8), g3((size_t)8 * 64 * 8, 0);
+  for (int o = 0; o < 16; ++o)
+    for (int st = 0; st < 2; ++st)
+      for (int l = 0; l < 64; ++l)
+        for (int e = 0; e < 8; ++e) {
+          const int i = l & 15, g = l >> 4;
+          g1[(((size_t)o * 2 + st) * 64 + l) * 8 + e] = w1[(size_t)(32 * st + 8 * g + e) * MLP_HID + 16 * o + i];
+        }
+  for (int o = 0; o < 16; ++o)
+    for (int st = 0; st < 8; ++st)
+      for (int l = 0; l < 64; ++l)
+        for (int e = 0; e < 8; ++e) {
+          const int i = l & 15, g = l >> 4;
+          g2[(((size_t)o * 8 + st) * 64 + l) * 8 + e] = w2[(size_t)kin16(st, e, g) * MLP_HID + 16 * o + i];
+        }
+  for (int st = 0; st < 8; ++st)
+    for (int l = 0; l < 64; ++l)
+      for (int e = 0; e < 8; ++e) {
+        const int i = l & 15, g = l >> 4;
+        if (i < MLP_OUT) g3[((size_t)st * 64 + l) * 8 + e] = w3[(size_t)kin16(st, e, g) * MLP_OUT + i];
+      }
   std::vector<float> bias(MLP_HID * 2 + 32);  // b3 zero-padded to one 32-row tile
   std::memcpy(bias.data(), b1, MLP_HID * 4);
   std::memcpy(bias.data() + MLP_HID, b2, MLP_HID * 4);
@@ -2097,6 +2128,9 @@ int ccka_mlp_set_weights(ccka_ctx* c, int32_t in_dim, int32_t hidden, int32_t ou
   if ((rc = dupload(c, c->d_mb, bias.data(), bias.size())) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_w2b, (const mlp_bf16x8*)f2b.data(), f2b.size() / 8)) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_w3b, (const mlp_bf16x8*)f3b.data(), f3b.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w1g, (const mlp_bf16x8*)g1.data(), g1.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w2g, (const mlp_bf16x8*)g2.data(), g2.size() / 8)) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_w3g, (const mlp_bf16x8*)g3.data(), g3.size() / 8)) != CCKA_OK) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->mlp_have_w = true;
   return CCKA_OK;
@@ -2153,6 +2187,11 @@ int ccka_mlp_forward_async(ccka_ctx* c) {
   p.b3 = c->d_mb + 2 * MLP_HID;
   p.N = c->mlp_n;
   p.stamps = nullptr;
+  if (c->mlp_tile == 16) {
+    p.w1g = c->d_w1g;
+    p.w2g = c->d_w2g;
+    p.w3g = c->d_w3g;
+  }
   if (c->mlp_stamps) {
     if (!c->d_stamps && hipMalloc((void**)&c->d_stamps, 12 * sizeof(unsigned long long)) != hipSuccess)
       return fail(c, CCKA_ENOMEM, "stamps alloc");
@@ -2188,6 +2227,11 @@ int ccka_debug_mlp_batch(ccka_ctx* c, int32_t launches, double* avg_ms, double* 
   p.b3 = c->d_mb + 2 * MLP_HID;
   p.N = c->mlp_n;
   p.stamps = nullptr;
+  if (c->mlp_tile == 16) {
+    p.w1g = c->d_w1g;
+    p.w2g = c->d_w2g;
+    p.w3g = c->d_w3g;
+  }
   int rc = CCKA_OK;
   // the context's own pair spans the batch (ccka_sync / ccka_last_kernel_ms)
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -2347,6 +2391,13 @@ int ccka_debug_occ(ccka_ctx* c, int32_t occ) {
 
 // Internal: per-phase cycle totals of the last stamped rollout (ablate bit 16).
 // Internal: diagnostic phase stamps of the MLP kernel (read with ccka_debug_stamps).
+// Internal: the standalone forward's MFMA tile (16: mlp16_kernel, 32: mlp_kernel).
+int ccka_debug_mlp_tile(ccka_ctx* c, int32_t tile) {
+  if (!c || (tile != 16 && tile != 32)) return CCKA_EINVAL;
+  c->mlp_tile = tile;
+  return CCKA_OK;
+}
+
 int ccka_debug_mlp_stamps(ccka_ctx* c, int32_t enable) {
   if (!c) return CCKA_EINVAL;
   c->mlp_stamps = enable != 0;

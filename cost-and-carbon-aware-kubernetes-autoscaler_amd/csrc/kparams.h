@@ -306,6 +306,10 @@ struct MlpParams {
   const float *b1, *b2, *b3;
   int64_t N;
   unsigned long long* stamps;  // diagnostic phase stamps (nullptr in every real run)
+  // set: mlp16_kernel (v_mfma_f32_16x16x32_bf16) with these fragment arrays
+  const mlp_bf16x8* w1g;      // [16 row tiles][2 k-steps][64 lanes]
+  const mlp_bf16x8* w2g;      // [16][8][64] (k order of the chained 16x16 accumulators)
+  const mlp_bf16x8* w3g;      // [8][64], rows 8..15 zero
 };
 hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s);
 hipError_t launch_mlp_gen_states(uint16_t* x, int64_t count, uint64_t seed, hipStream_t s);

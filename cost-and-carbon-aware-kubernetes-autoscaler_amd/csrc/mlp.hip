@@ -258,6 +258,169 @@ __global__ void __launch_bounds__(256, 1) mlp_kernel(MlpParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same MLP on v_mfma_f32_16x16x32_bf16 (16-cycle issue; MI355X_MICROARCH.md
+// measures its loops at 1.12-1.15x the FLOP/s of 32x32x16 on random data, and
+// the 8-row output layer pads to 16 rows instead of 32). Transposed chaining as
+// in mlp_kernel, with the 16x16 layouts: the accumulator of output tile o
+// (16 units x 16 states) holds, in lane l, state l & 15 and units
+// 16o + 4(l >> 4) + 0..3; the B operand of a k-step holds state l & 15 and
+// k-slots 8(l >> 4) + e. Two consecutive accumulator tiles (2s, 2s+1), packed
+// to bf16, are k-step s of the next layer with the permuted k order
+// u = 32s + 16(e >> 2) + 4(l >> 4) + (e & 3) (mlp16 fragments on the host).
+// One persistent 4-wave workgroup per CU; W1 fragments in accumulation
+// registers, W2 / W3 fragments and the biases in LDS (138 KiB); each wave
+// evaluates T16 16-state tiles per pass (every W2 fragment read feeds T16
+// MFMAs), the next pass's states in flight during layers 2 and 3.
+// ---------------------------------------------------------------------------
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4v mfma16(const bf16x8& a, const bf16x8& b, const f32x4v& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// tiles (2s, 2s+1) -> one bf16 B fragment with ReLU (as relu_pack)
+__device__ __forceinline__ bf16x8 relu_pack2(const f32x4v& a, const f32x4v& b) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; j += 2) {
+    const bf16x2v x = __builtin_convertvector((f32x2){a[j], a[j + 1]}, bf16x2v);
+    const short2v v = __builtin_elementwise_max(__builtin_bit_cast(short2v, x), (short2v){0, 0});
+    r[j] = v.x;
+    r[j + 1] = v.y;
+    const bf16x2v y = __builtin_convertvector((f32x2){b[j], b[j + 1]}, bf16x2v);
+    const short2v w = __builtin_elementwise_max(__builtin_bit_cast(short2v, y), (short2v){0, 0});
+    r[4 + j] = w.x;
+    r[4 + j + 1] = w.y;
+  }
+  return r;
+}
+#ifndef MLP16_T
+#define MLP16_T 4
+#endif
+constexpr int T16 = MLP16_T;  // 16-state tiles per wave and pass
+__global__ void __launch_bounds__(256, 1) mlp16_kernel(MlpParams p) {
+  constexpr int NO = MLP_HID / 16;                      // output tiles of layers 1 and 2
+  constexpr int KS1 = MLP_IN / 32, KS2 = MLP_HID / 32;  // k-steps
+  constexpr int PF = 2;                                 // W2 fragments in flight
+  __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 16];  // b1 | b2 | b3 (zero-padded to 16)
+  __shared__ bf16x8 s_w3[KS2 * WAVE];                                   // 8 KiB
+  __shared__ bf16x8 s_w2[NO * KS2 * WAVE];                              // 128 KiB
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+  const int j = lane & 15, g = lane >> 4;
+  for (int x = tid; x < NO * KS2 * WAVE; x += blockDim.x) s_w2[x] = p.w2g[x];
+  for (int x = tid; x < KS2 * WAVE; x += blockDim.x) s_w3[x] = p.w3g[x];
+  for (int x = tid; x < 2 * MLP_HID + 16; x += blockDim.x) s_b[x] = x < 2 * MLP_HID + MLP_OUT ? p.b1[x] : 0.f;
+  bf16x8 w1[NO][KS1];
+#pragma unroll
+  for (int o = 0; o < NO; ++o)
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      w1[o][s] = p.w1g[(o * KS1 + s) * WAVE + lane];
+      asm volatile("" : "+a"(w1[o][s]));  // accumulation registers: MFMA reads its A operand from them
+    }
+  __syncthreads();
+  auto bias4 = [&](int off) { return *reinterpret_cast<const f32x4v*>(s_b + off + 4 * g); };
+  const int64_t ntiles = (p.N + 15) / 16, npass = (ntiles + T16 - 1) / T16;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / WAVE);
+  int64_t pass = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wave;
+  // X^T fragments (B operand of layer 1): state j of the tile, features 32s + 8g .. +7
+  auto load_x = [&](int64_t tl, bf16x8* xf) {
+    const int64_t row = tl * 16 + j;
+    const bool ok = row < p.N;
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(p.x + (ok ? row : 0) * MLP_IN + 8 * g);
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      const bf16x8 v = src[4 * s];
+      xf[s] = ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  bf16x8 x[T16][KS1];
+#pragma unroll
+  for (int t = 0; t < T16; ++t) load_x(pass * T16 + t, x[t]);
+  for (; pass < npass; pass += nw) {
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- layer 1: H1^T = relu(W1^T X^T + b1). The tile pair (2m, 2m+1) is
+    // packed to bf16 during tile 2m+2's MFMAs (its epilogue in their shadow) ----
+    bf16x8 h1[T16][KS2];
+    {
+      f32x4v pa[T16], pb[T16], c[T16];
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        const f32x4v b = bias4(16 * o);
+#pragma unroll
+        for (int s = 0; s < KS1; ++s) {
+#pragma unroll
+          for (int t = 0; t < T16; ++t) c[t] = mfma16(w1[o][s], x[t][s], s == 0 ? b : c[t]);
+          if (o >= 2 && !(o & 1)) {  // the pending pair (o - 2, o - 1), half of its tiles per k-step
+#pragma unroll
+            for (int t = s * T16 / KS1; t < (s + 1) * T16 / KS1; ++t) h1[t][(o >> 1) - 1] = relu_pack2(pa[t], pb[t]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int t = 0; t < T16; ++t) {
+          if (o & 1) pb[t] = c[t];
+          else pa[t] = c[t];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < T16; ++t) h1[t][KS2 - 1] = relu_pack2(pa[t], pb[t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the next pass's states in flight during layers 2 and 3
+#pragma unroll
+    for (int t = 0; t < T16; ++t) load_x((pass + nw) * T16 + t, x[t]);
+    // ---- layers 2 and 3: H2^T = relu(W2^T H1^T + b2) tile by tile, W2
+    // fragments PF k-steps ahead; the pair (2m, 2m+1) is packed and multiplied
+    // into Y^T = W3^T H2^T + b3 (k-step m) during tile 2m+2's MFMAs ----
+    f32x4v y[T16];
+    {
+      const f32x4v b3 = bias4(2 * MLP_HID);
+#pragma unroll
+      for (int t = 0; t < T16; ++t) y[t] = b3;
+    }
+    {
+      f32x4v pa[T16], pb[T16], c[T16];
+      bf16x8 wq[PF + 1];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) wq[q] = s_w2[q * WAVE + lane];
+      bf16x8 w3 = s_w3[lane];
+#pragma unroll
+      for (int o = 0; o < NO; ++o) {
+        const f32x4v b = bias4(MLP_HID + 16 * o);
+        if (o >= 2 && !(o & 1)) w3 = s_w3[((o >> 1) - 1) * WAVE + lane];
+#pragma unroll
+        for (int s = 0; s < KS2; ++s) {
+          const int q = o * KS2 + s;
+          if (q + PF < NO * KS2) wq[(q + PF) % (PF + 1)] = s_w2[(q + PF) * WAVE + lane];
+          const bf16x8 w = wq[q % (PF + 1)];
+#pragma unroll
+          for (int t = 0; t < T16; ++t) c[t] = mfma16(w, h1[t][s], s == 0 ? b : c[t]);
+          if (o >= 2 && !(o & 1) && s >= 1 && s <= T16) {
+            const int t = s - 1;
+            y[t] = mfma16(w3, relu_pack2(pa[t], pb[t]), y[t]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int t = 0; t < T16; ++t) {
+          if (o & 1) pb[t] = c[t];
+          else pa[t] = c[t];
+        }
+      }
+      w3 = s_w3[(KS2 - 1) * WAVE + lane];
+#pragma unroll
+      for (int t = 0; t < T16; ++t) y[t] = mfma16(w3, relu_pack2(pa[t], pb[t]), y[t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // rows 4g..4g+3 of Y^T = actions 4g..4g+3 of state j (g < 2)
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+      const int64_t row = (pass * T16 + t) * 16 + j;
+      if (g < 2 && row < p.N) *reinterpret_cast<f32x4v*>(p.y + row * MLP_OUT + 4 * g) = y[t];
+    }
+  }
+}
+
 // Synthetic cluster states: Irwin-Hall sums of Philox words (~N(0,1)), bf16.
 __device__ __forceinline__ void philox_s(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                          uint32_t k1, uint32_t out[4]) {
@@ -284,6 +447,7 @@ __global__ void __launch_bounds__(256) mlp_gen_states_kernel(uint16_t* x, int64_
 
 hipError_t launch_mlp(const MlpParams& p, int cus, hipStream_t s) {
   if (p.stamps) hipLaunchKernelGGL(mlp_kernel<true>, dim3((unsigned)cus), dim3(256), 0, s, p);
+  else if (p.w1g) hipLaunchKernelGGL(mlp16_kernel, dim3((unsigned)cus), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(mlp_kernel<false>, dim3((unsigned)cus), dim3(256), 0, s, p);
   return hipGetLastError();
 }

@@ -3,7 +3,8 @@ rollout_d1.hip: D1_S_V quiet steps per iteration, D1_K_V event cadence,
 D1_VMN_V trace rows in flight, D1_LEAN_V default-behavior quiet path, D1_NT_V /
 D1_NTL_V streaming hints) as separate libccka.so copies under csrc/build/variants/<name>/,
 linked with the main build's other objects. Profiling aid only.
-NAME=r@other.hip replaces rollout.hip (the general kernel) instead, NAME=p@other.hip pg.hip.
+NAME=r@other.hip replaces rollout.hip (the general kernel) instead, NAME=p@other.hip pg.hip, NAME=m@other.hip
+mlp.hip (NAME=m@mlp.hip:-DX builds mlp.hip itself with extra flags).
 usage: python tools/build_variants.py name=-DD1_S_V=3 [name2="-DA -DB" ...]"""
 import os
 import subprocess
@@ -22,6 +23,8 @@ for arg in sys.argv[1:]:
         defs, base, extra = defs[1:], "rollout.o", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
     elif defs.startswith("p@"):  # the policy-gradient kernels' source
         defs, base, extra = defs[1:], "pg.o", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+    elif defs.startswith("m@"):  # the MLP kernels' source
+        defs, base, extra = defs[1:], "mlp.o", ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
     if defs.startswith("@"):  # NAME=@other.hip[:flags]: another source file in csrc/ (e.g. a committed version)
         src, _, defs = defs[1:].partition(":")
     out = os.path.join(CSRC, "build", "variants", name)
