@@ -513,6 +513,10 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
   }
   return y;
 }
+// the exact disruption gate of one-deployment worlds (0: the A/B variant)
+#ifndef G_GATE_V
+#define G_GATE_V 1
+#endif
 // v_permlane32_swap_b32: x's lanes 32..63 <-> y's lanes 0..31
 // (tools/probe/permlane.hip documents the lanes). Only for operands held in
 // separate scalars: ROCm 7.2 lowers a swap of two elements of one MFMA
@@ -1481,7 +1485,46 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 
     if (active) {
       // ---- G. disruption (skipped exactly when nothing it depends on moved) ----
-      if ((g_dirty || t >= g_wake) && !(p.ablate & 1)) {
+      const bool g_eval = (g_dirty || t >= g_wake) && !(p.ablate & 1);
+      // One deployment without drift / replacement / multi-node consolidation:
+      // an exact gate first (the single-deployment kernel's). The phase acts
+      // only on a ready candidate past its consolidateAfter that is empty, or
+      // of a WhenEmptyOrUnderutilized pool with its pods fitting the other
+      // compatible ready slots (their free capacity F minus its own >= its
+      // pods; the budget and the PDB only restrict further); with none, the
+      // evaluation would change nothing, so only the next wake step is kept.
+      bool g_gate = true;
+      if constexpr (DMAX == 1) {
+        if (G_GATE_V && g_eval && !gdrift && !greplace && !gmulti) {
+          int F = 0;
+          uint32_t cm1 = 0, el = 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            const uint32_t x = ninfo[n];
+            const bool r = (used & rdy) >> n & 1u;
+            const bool c = r && (capbit(ni_cap(x)) & capsel[0]);
+            cm1 |= (c ? 1u : 0u) << n;
+            F += c ? ncap[n] - npods[n][0] : 0;
+            int ca = 0, pol = 0;
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q)
+              if (q == ni_pool(x)) { ca = pca[q]; pol = ppol[q]; }
+            const bool cand = r && (t - nlast[n]) * CCKA_STEP_SECONDS >= ca &&
+                              (npods[n][0] == 0 || pol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED);
+            el |= (cand ? 1u : 0u) << n;
+          }
+          bool any = false;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            const int pods = npods[n][0];
+            const int fo = F - ((cm1 >> n & 1u) ? ncap[n] - pods : 0);
+            any |= (el >> n & 1u) && (pods == 0 || fo >= pods);
+          }
+          g_gate = any;
+        }
+      }
+      if (g_eval && !g_gate) g_dirty = false;
+      if (g_eval && g_gate) {
         bool budget_hit = false, any_deleted = false;
         long long allowed = 0x3fffffffffffffffLL;
         if (pdb_pct >= 0) {
@@ -2242,6 +2285,8 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #pragma unroll
         for (int n = 0; n < MAXN; ++n) pending_repl |= nsrc[n] != 0;
         g_dirty = budget_hit || any_deleted || dmask != 0 || pending_repl;
+      }
+      if (g_eval) {
         // next step at which a node becomes a new candidate (consolidatable and ready)
         int wake = 0x7fffffff;
 #pragma unroll
