@@ -130,10 +130,8 @@ constexpr int kPartBytes = 11 * 8;
 
 // kernel instantiation chosen for (D, max_nodes): DMAX x MAXN
 inline void kernel_dims(int D, int maxn, int* dmax, int* nmax) {
-  if (D == 1 && maxn <= 8) { *dmax = 1; *nmax = 8; }
-  else if (D == 1) { *dmax = 1; *nmax = 16; }
-  else if (D <= 4) { *dmax = 4; *nmax = 16; }
-  else { *dmax = 16; *nmax = 16; }
+  *dmax = D == 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : 16;
+  *nmax = maxn <= 8 && *dmax <= 4 ? 8 : 16;
 }
 
 hipError_t launch_gen_load(const GenParams& g, hipStream_t s);

@@ -1522,6 +1522,67 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           }
           g_gate = any;
         }
+      } else {
+        // Several deployments (same cases): a necessary condition for a
+        // deletion. A non-empty candidate's pods move onto ready nodes of a
+        // capacity type one of its deployments admits, so their CPU, memory and
+        // pod count must fit those nodes' free resources (the candidate's own
+        // excluded); with no candidate that is empty or passes these sums, the
+        // sequential search would reject every one.
+        if (G_GATE_V && g_eval && !gdrift && !greplace && !gmulti) {
+          auto node_use = [&](int n, int& c, int& m, int& pods) {
+            c = 0; m = 0; pods = 0;
+#pragma unroll
+            for (int e = 0; e < DMAX; ++e) {
+              const int k = e < D ? npods[n][e] : 0;
+              c += k * dep[e].req_cpu;
+              m += k * dep[e].req_mem;
+              pods += k;
+            }
+          };
+          int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;  // free resources by capacity type
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (!(rdy >> n & 1u)) continue;
+            int c, m, pods;
+            node_use(n, c, m, pods);
+            const ccka_itype& ty = L.types[ni_type(ninfo[n])];
+            const bool od = ni_cap(ninfo[n]) != 0;
+            const int fc = ty.alloc_cpu_m - c, fmm = ty.alloc_mem_mi - m, fp = ty.max_pods - pods;
+            ac0 += od ? 0 : fc; ac1 += od ? fc : 0;
+            am0 += od ? 0 : fmm; am1 += od ? fmm : 0;
+            ap0 += od ? 0 : fp; ap1 += od ? fp : 0;
+          }
+          bool any = false;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (!(rdy >> n & 1u)) continue;
+            const uint32_t x = ninfo[n];
+            int ca = 0, pol = 0;
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q)
+              if (q == ni_pool(x)) { ca = pca[q]; pol = ppol[q]; }
+            if ((t - nlast[n]) * CCKA_STEP_SECONDS < ca) continue;
+            int c, m, pods;
+            node_use(n, c, m, pods);
+            if (pods == 0) { any = true; continue; }
+            if (pol != CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) continue;
+            uint32_t cs = 0;  // capacity types some deployment with pods here admits
+#pragma unroll
+            for (int e = 0; e < DMAX; ++e) cs |= (e < D && npods[n][e] > 0) ? capsel[e] : 0u;
+            const bool s0 = (cs & capbit(0)) != 0, s1 = (cs & capbit(1)) != 0;
+            int vc = (s0 ? ac0 : 0) + (s1 ? ac1 : 0), vm = (s0 ? am0 : 0) + (s1 ? am1 : 0);
+            int vp = (s0 ? ap0 : 0) + (s1 ? ap1 : 0);
+            if (cs & capbit(ni_cap(x))) {  // not a receiver of its own pods
+              const ccka_itype& ty = L.types[ni_type(x)];
+              vc -= ty.alloc_cpu_m - c;
+              vm -= ty.alloc_mem_mi - m;
+              vp -= ty.max_pods - pods;
+            }
+            any |= c <= vc && m <= vm && pods <= vp;
+          }
+          g_gate = any;
+        }
       }
       if (g_eval && !g_gate) g_dirty = false;
       if (g_eval && g_gate) {
@@ -2519,12 +2580,23 @@ hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s
   (void)grid; (void)lds; (void)s;
   return hipErrorInvalidValue;
 #else
-  if (p.D == 1 && p.maxn <= 8)
+  // the smallest instantiation that holds the world (kernel_dims)
+  int dmax, nmax;
+  kernel_dims(p.D, p.maxn, &dmax, &nmax);
+  if (dmax == 1 && nmax == 8)
     hipLaunchKernelGGL((rollout_kernel<1, 8>), dim3(grid), dim3(block), lds, s, p);
-  else if (p.D == 1)
+  else if (dmax == 1)
     hipLaunchKernelGGL((rollout_kernel<1, 16>), dim3(grid), dim3(block), lds, s, p);
-  else if (p.D <= 4)
+  else if (dmax == 2 && nmax == 8)
+    hipLaunchKernelGGL((rollout_kernel<2, 8>), dim3(grid), dim3(block), lds, s, p);
+  else if (dmax == 2)
+    hipLaunchKernelGGL((rollout_kernel<2, 16>), dim3(grid), dim3(block), lds, s, p);
+  else if (dmax == 4 && nmax == 8)
+    hipLaunchKernelGGL((rollout_kernel<4, 8>), dim3(grid), dim3(block), lds, s, p);
+  else if (dmax == 4)
     hipLaunchKernelGGL((rollout_kernel<4, 16>), dim3(grid), dim3(block), lds, s, p);
+  else if (dmax == 8)
+    hipLaunchKernelGGL((rollout_kernel<8, 16>), dim3(grid), dim3(block), lds, s, p);
   else
     hipLaunchKernelGGL((rollout_kernel<16, 16>), dim3(grid), dim3(block), lds, s, p);
   return hipGetLastError();
