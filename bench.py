@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--multi", action="store_true",
                     help="configs 2-4 with multi-node consolidation (SEMANTICS 3.G3, Karpenter's default for "
                          "WhenEmptyOrUnderutilized pools)")
+    ap.add_argument("--deployments", type=int, default=1,
+                    help="config 2 with this many HPA deployments sharing each cluster's nodes (the general "
+                         "kernel's multi-deployment layouts; 8 node slots up to 2 deployments, else 16)")
     ap.add_argument("--keda", action="store_true",
                     help="configs 2-3 with a KEDA ScaledObject queue worker instead of the HPA deployment "
                          "(SURVEY A.2 defaults: scale from / to zero, cooldown 300 s, min 0, max 100; threshold "
@@ -190,6 +193,11 @@ def main():
             sc = configs.config4_scenarios(rank * grids, grids, ntr)
             gen = configs.config4_trace_gen()
             traj = (args.mode or "summary") == "trajectory"
+        if args.deployments > 1:  # several HPA deployments per cluster (demo_30's burst shape)
+            spec.deploys = [configs.deployment(abi.SCALER_HPA, replicas0=3, max_r=30,
+                                               req_cpu=(200, 300, 250, 400)[d % 4], target=(70, 60, 80, 50)[d % 4])
+                            for d in range(args.deployments)]
+            spec.max_nodes = 8 if args.deployments <= 2 else 16
         if args.keda:  # the queue-worker side of the path: one ScaledObject per scenario
             spec.deploys = [configs.deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=500, keda_activation=0,
                                                keda_cooldown=300, keda_min=0, keda_max=100)]
@@ -320,10 +328,11 @@ def main():
         # the 1024 shared traces), trajectory 16 B per cluster-step written once
         # (trajectory mode), per-scenario params (6 B) read and results (72 B)
         # written once
-        load_cols = configs.CONFIG4_TRACES if cfg == 4 else N
+        load_cols = (configs.CONFIG4_TRACES if cfg == 4 else N) * len(spec.deploys)
         bytes_launch = load_cols * T * 4 + (N * T * 16 if traj else 0) + N * 6 + N * 72
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
         traffic, traffic_src = (None, None) if (args.drift or args.replace or args.multi or args.keda or
+                                                args.deployments > 1 or
                                                 args.hpa_sync not in (0, 60) or args.budget is not None or
                                                 args.trace_flat) else measured_traffic(cfg, traj, N, T)
         workloads = {
@@ -341,11 +350,14 @@ def main():
             "scaling": "strong" if cfg == 3 else "weak", "vs_baseline": None, "dtype": "int32+int64+f64",
             "data": "synthetic (on-device Philox load traces, seed 20251205)",
             "config": {"workload": (workloads[cfg].replace("HPA", "KEDA ScaledObject (scale to zero)") if args.keda
-                                    else workloads[cfg]) + (" + Karpenter drift at the zone switch" if args.drift else "")
+                                    else workloads[cfg].replace("1 deployment", f"{args.deployments} HPA deployments "
+                                                                f"sharing {spec.max_nodes} node slots")
+                                    if args.deployments > 1 else workloads[cfg]) + (" + Karpenter drift at the zone switch" if args.drift else "")
                        + (" + replacement consolidation" if args.replace else "")
                        + (" + multi-node consolidation" if args.multi else "")
                        + (f" + HPA sync every {args.hpa_sync} s" if args.hpa_sync not in (0, 60) else "")
-                       + (f", disruption budget {args.budget} %" if args.budget is not None else ""),
+                       + (f", disruption budget {args.budget} %" if args.budget is not None else "")
+,
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
                        "trace_layout": "[T][N] (shared traces)" if cfg == 4 else "[T][N]" if args.trace_flat else "wave-tiled [wave][T][lanes] (built by the first rollout)",
@@ -356,7 +368,7 @@ def main():
                          # not measured in this run: copied from the committed profile named here
                          "traffic_source": traffic_src,
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else
-                                   f"rollout_kernel<{len(spec.deploys)},{spec.max_nodes}>",
+                                   "rollout_kernel<%d,%d>" % general_dims(len(spec.deploys), spec.max_nodes),
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},
             # the kernel is issue-bound, not HBM-bound: its measured issue-side
@@ -393,6 +405,13 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def general_dims(d, maxn):
+    """The general kernel's register layout for d deployments and maxn node
+    slots (kernel_dims in csrc/kparams.h)."""
+    dmax = 1 if d == 1 else 2 if d <= 2 else 4 if d <= 4 else 8 if d <= 8 else 16
+    return dmax, 8 if maxn <= 8 and dmax <= 4 else 16
 
 
 def measured_traffic(cfg, traj, n, T):
