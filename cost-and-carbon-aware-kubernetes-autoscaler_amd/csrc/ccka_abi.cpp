@@ -1130,6 +1130,13 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
   } else {
     k.ptable = nullptr;  // the argmin-table launches are the policy loops' (weights k / 16)
     k.pjtab = nullptr;
+    k.stamps = nullptr;
+    if (k.ablate & 16) {  // diagnostic phase stamps (read by ccka_debug_stamps; GK_STAMPS builds)
+      if (!c->d_stamps && hipMalloc((void**)&c->d_stamps, 12 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(c, CCKA_ENOMEM, "stamps alloc");
+      HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, 12 * sizeof(unsigned long long), c->stream));
+      k.stamps = c->d_stamps;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
     HIPCHK(c, launch_rollout(k, block, lds, c->stream));
@@ -1353,6 +1360,15 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
         k.pol_act = nullptr;
         k.feat_rec = nullptr;
       };
+      k.stamps = nullptr;
+      if (k.ablate & 16) {  // diagnostic phase stamps (GK_STAMPS builds; ccka_debug_stamps)
+        if (!c->d_stamps && hipMalloc((void**)&c->d_stamps, 12 * sizeof(unsigned long long)) != hipSuccess) {
+          clear_fused();
+          return fail(c, CCKA_ENOMEM, "stamps alloc");
+        }
+        HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, 12 * sizeof(unsigned long long), c->stream));
+        k.stamps = c->d_stamps;
+      }
       hipError_t le = hipEventRecord(c->ev0, c->stream);
       k.ptable = nullptr;
       if (le == hipSuccess && !c->pol_table_off && (rc = policy_tables(c, &k)) != CCKA_OK) {

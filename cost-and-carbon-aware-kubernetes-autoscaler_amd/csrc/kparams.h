@@ -76,6 +76,7 @@ struct KParams {
   int32_t T, D, K, Z, R, P, maxn, span, all_hours;
   int32_t lds_off_cap1, lds_off_tile, lds_off_claims, lds_off_misc, lds_off_ci;
   int32_t ablate;  // profiling-only phase switches (0 in every real run)
+  unsigned long long* stamps;  // diagnostic phase cycle totals (GK_STAMPS builds only; nullptr otherwise)
   int32_t prov[CCKA_MAX_DEPLOY];
   // fused closed loop (rollout_kernel<1, 8, POL>): the MLP runs inside the step
   // loop (SEMANTICS 5); POL 1 = deterministic actions, 2 = sampled (the

@@ -433,6 +433,10 @@ __device__ int behavior_long(const ccka_hpa_rules* up, const ccka_hpa_rules* dn,
   return rc < lo ? lo : (rc > hi ? hi : rc);
 }
 
+// W2 fragments the fused loop's MLP reads ahead of their MFMA (A/B macro)
+#ifndef MLP_W2PF
+#define MLP_W2PF 2
+#endif
 // ---- the learned policy inside the step loop (fused closed loop, POL > 0) ----
 // The MLP of mlp.hip (H1^T = W1^T X^T, H2^T = W2^T H1^T, Y^T = W3^T H2^T on
 // v_mfma_f32_32x32x16_bf16, each accumulator chained as the next layer's B
@@ -478,14 +482,16 @@ __device__ __forceinline__ pf32x16 pbias_tile(const float* b, int h) {
 // result = outputs 4h..4h+3 of the lane's column state. W1 fragments come
 // from L2 one row block ahead (their latency hides under the block's MFMAs
 // and epilogue), W2 / W3 fragments and the biases from LDS.
+// w1b0: W1's first row block, loaded by the caller ahead of the tile; the
+// call reloads it into w1b0 during its second layer for the next tile
 __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], const pbf16x8* __restrict__ w1f,
-                                            const pbf16x8* s_w2, const pbf16x8* s_w3, const float* s_b, int lane,
-                                            int h) {
+                                            pbf16x8 (&w1b0)[MLP_IN / 16], const pbf16x8* s_w2, const pbf16x8* s_w3,
+                                            const float* s_b, int lane, int h) {
   constexpr int KS1 = MLP_IN / 16, KS2 = MLP_HID / 16, NB = MLP_HID / 32;
   pbf16x8 hh[KS2];
   pbf16x8 wc[KS1], wn[KS1];
 #pragma unroll
-  for (int s = 0; s < KS1; ++s) wc[s] = w1f[s * 64 + lane];
+  for (int s = 0; s < KS1; ++s) wc[s] = w1b0[s];
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     if (n + 1 < NB) {
@@ -501,14 +507,28 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
     for (int s = 0; s < KS1; ++s) wc[s] = wn[s];
     __builtin_amdgcn_sched_barrier(0);  // bounded live ranges: the rollout state shares the register file
   }
+#pragma unroll
+  for (int s = 0; s < KS1; ++s) w1b0[s] = w1f[s * 64 + lane];  // the next tile's (L2 latency under layer 2)
   pf32x16 y = pbias_tile(s_b + 2 * MLP_HID, h);
+  // W2 fragments from LDS MLP_W2PF MFMAs ahead (one wave per SIMD: nothing
+  // else hides an LDS read issued just before its MFMA)
+  constexpr int PF = MLP_W2PF;
+  pbf16x8 wq[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) wq[j] = s_w2[j * 64 + lane];
 #pragma unroll
   for (int m = 0; m < NB; ++m) {
     pf32x16 c = pbias_tile(s_b + MLP_HID + 32 * m, h);
+    const pbf16x8 w3a = s_w3[(2 * m) * 64 + lane], w3b = s_w3[(2 * m + 1) * 64 + lane];  // used after the chain
 #pragma unroll
-    for (int kk = 0; kk < KS2; ++kk) c = pmfma(s_w2[(m * KS2 + kk) * 64 + lane], hh[kk], c);
-    y = pmfma(s_w3[(2 * m) * 64 + lane], prelu_pack(c, 0), y);
-    y = pmfma(s_w3[(2 * m + 1) * 64 + lane], prelu_pack(c, 1), y);
+    for (int kk = 0; kk < KS2; ++kk) {
+      const pbf16x8 w = wq[kk % PF];
+      const int nx = m * KS2 + kk + PF;  // the fragment PF ahead (across m-blocks)
+      if (nx < NB * KS2) wq[kk % PF] = s_w2[nx * 64 + lane];
+      c = pmfma(w, hh[kk], c);
+    }
+    y = pmfma(w3a, prelu_pack(c, 0), y);
+    y = pmfma(w3b, prelu_pack(c, 1), y);
     __builtin_amdgcn_sched_barrier(0);
   }
   return y;
@@ -540,6 +560,23 @@ __device__ __forceinline__ void pol_philox(uint32_t c0, uint32_t c1, uint32_t c2
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 }  // namespace
+
+// Diagnostic phase stamps (tools/build_variants.py NAME="r@rollout.hip:-DGK_STAMPS",
+// tools/gk_stamps.py): s_memtime deltas per phase of the step loop
+// accumulated per wave, at wave-uniform points
+#ifdef GK_STAMPS
+constexpr bool kGKS = true;
+#else
+constexpr bool kGKS = false;
+#endif
+#define GK_STAMP(k)                                             \
+  do {                                                          \
+    if constexpr (kGKS) {                                       \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+      gst[k] += now_ - glast;                                   \
+      glast = now_;                                             \
+    }                                                           \
+  } while (0)
 
 // POL: 0 = rule-based rollout (steps [t0, t1), resumable); 1 / 2 = the fused
 // closed loop over the whole horizon: before every step the scenario's
@@ -861,7 +898,6 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #pragma unroll
     for (int d = 0; d < DMAX; ++d)
       if (d < D) { reps += replicas[d]; rd += rpods[d]; }
-    const int tf = min(tq, p.T - 1);
     const int mf = (gw->start_minute + tq) % 1440, hf = mf / 60;
     const bool pk = pswitch && (ps <= pe ? (mf >= ps && mf < pe) : (mf >= ps || mf < pe));
     uint16_t f[64];
@@ -869,7 +905,9 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     f[1] = f2bf((float)reps * 0.0625f);
     f[2] = f2bf((float)rd * 0.0625f);
     f[3] = f2bf((float)(reps - rd) * 0.0625f);
-    f[4] = f2bf((float)lptr[((int64_t)tf * D) * lstride] * (1.0f / 1024.0f));
+    // the sample of step min(tq, T - 1): Lnext[0] holds it at the top of step
+    // tq and after the last one (no second load of the same word)
+    f[4] = f2bf((float)Lnext[0] * (1.0f / 1024.0f));
     f[5] = f2bf((float)nsp);
     f[6] = f2bf((float)nod);
     f[7] = f2bf(pk ? 1.0f : 0.0f);
@@ -897,9 +935,13 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     for (int q = 0; q < 8; ++q) dst[q] = make_uint4(fw[4 * q], fw[4 * q + 1], fw[4 * q + 2], fw[4 * q + 3]);
   };
 
+  unsigned long long gst[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, glast = kGKS ? __builtin_amdgcn_s_memtime() : 0ull;
   for (int t = t0; t < t1; ++t, minute = minute == 1439 ? 0 : minute + 1) {
     if constexpr (POL != 0) {
       // ---- the learned policy chooses step t's HPA target and carbon weight ----
+      pbf16x8 w1b0[MLP_IN / 16];  // W1's first row block, in flight under the features
+#pragma unroll
+      for (int s = 0; s < MLP_IN / 16; ++s) w1b0[s] = p.w1f[s * 64 + lane];
       uint32_t fw[32];
       feat_words(t, fw);
       if (p.feat_rec && active) store_feat(p.feat_rec + ((int64_t)t * p.N + i) * 64, fw);
@@ -920,13 +962,16 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         xb[s] = __builtin_bit_cast(pbf16x8, make_uint4(wb[0], wb[1], wb[2], wb[3]));
       }
       const int hl = lane >> 5;
+      GK_STAMP(7);  // features, X^T operands
       pf32x16 ya, yb;
       if (p.ablate & 32) {  // profiling only: the loop without its MLP
 #pragma unroll
         for (int k = 0; k < 16; ++k) ya[k] = yb[k] = 0.f;
       } else {
-        ya = mlp_tile(xa, p.w1f, s_w2, s_w3, s_mb, lane, hl);
-        yb = mlp_tile(xb, p.w1f, s_w2, s_w3, s_mb, lane, hl);
+        ya = mlp_tile(xa, p.w1f, w1b0, s_w2, s_w3, s_mb, lane, hl);
+        GK_STAMP(8);  // MLP tile a
+        yb = mlp_tile(xb, p.w1f, w1b0, s_w2, s_w3, s_mb, lane, hl);
+        GK_STAMP(9);  // MLP tile b
       }
       // this lane's state's 8 outputs
       float y[MLP_OUT] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -984,6 +1029,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         }
       }
     }
+    GK_STAMP(10);  // the fused loop's action
     int Lcur[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
@@ -1041,6 +1087,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; pend[d] = 0; kact_any[d] = false; }
 
+    GK_STAMP(0);  // samples, the hour's tiles
     if (active) {
       // ---- B. readiness transitions (nominated pods start running) ----
       if (t >= next_ready) {
@@ -1077,6 +1124,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           if (x.cap_mask) pcm[q] = x.cap_mask;
         }
       }
+      GK_STAMP(1);  // readiness, profile
       // ---- C. scalers: nsub decisions on the step's metric sample ----
       for (int sub = 0; sub < p.nsub; ++sub) {
       if (sub > 0) {
@@ -1201,6 +1249,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       }
       if (p.hlen) hpos = hpos + 1 == p.hlen ? 0 : hpos + 1;
       }  // sub-steps
+      GK_STAMP(2);  // scalers
       // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
@@ -1275,6 +1324,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       }
     }
 
+    GK_STAMP(3);  // reconcile, scheduler
     // ---- F2. Karpenter provisioning ----
     if (POL > 0 && p.ptable) {
       // the fused closed loop on a single-deployment world without pool limits:
@@ -1483,6 +1533,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       }
     }
 
+    GK_STAMP(4);  // provisioning
     if (active) {
       // ---- G. disruption (skipped exactly when nothing it depends on moved) ----
       const bool g_eval = (g_dirty || t >= g_wake) && !(p.ablate & 1);
@@ -2362,6 +2413,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         }
         g_wake = wake;
       }
+      GK_STAMP(5);  // disruption
       // ---- H. accounting ----
       long long upp[DMAX];
 #pragma unroll
@@ -2437,6 +2489,14 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         rcd.flags = (uint16_t)flags;
         *reinterpret_cast<int4*>(&p.traj[(int64_t)t * p.N + i]) = *reinterpret_cast<int4*>(&rcd);
       }
+    }
+    GK_STAMP(6);  // accounting, record
+  }
+  if constexpr (kGKS) {
+    if (p.stamps && lane == (__ffsll((long long)__ballot(1)) - 1)) {
+#pragma unroll
+      for (int k = 0; k < 11; ++k) atomicAdd(&p.stamps[k], gst[k]);
+      atomicAdd(&p.stamps[11], 1ull);  // waves
     }
   }
   if (!active) return;

@@ -12,7 +12,7 @@ from ccka import abi, configs  # noqa: E402
 from ccka.engine import Engine  # noqa: E402
 from ccka.world import deployment  # noqa: E402
 
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+N = int(sys.argv[1]) if len(sys.argv) > 1 and __name__ == "__main__" else 100_000
 
 
 def hpa_mix(d, max_nodes):
@@ -37,29 +37,37 @@ worlds = {
     "hpa4_16": lambda: hpa_mix(4, 16),
     "hpa12_16": lambda: hpa_mix(12, 16),
 }
-names = sys.argv[2:] or list(worlds)
-LIB = os.environ.get("VARIANT")  # a tools/build_variants.py variant instead of the main build
-e = Engine(0, lib_path=os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build",
-                                    "variants", LIB, "libccka.so") if LIB else None)
-import ctypes as C  # noqa: E402
-e.lib.ccka_debug_engine.argtypes = [C.c_void_p, C.c_int32]
-e.lib.ccka_debug_engine(e.ctx, 1)  # the general kernel for every world
-ABL = [int(x) for x in os.environ.get("ABLATE", "0").split(",")]  # profiling: ccka_debug_ablate masks
-e.lib.ccka_debug_ablate.argtypes = [C.c_void_p, C.c_int32]
-for name, abl in [(n, a) for n in names for a in ABL]:
-    e.lib.ccka_debug_ablate(e.ctx, abl)
-    w = worlds[name]()
-    e.set_world(w)
-    e.set_scenarios(configs.hpa_scenarios(N))
-    e.gen_load(configs.trace_gen())
-    t0 = time.time()
-    e.rollout(trajectory=False)
-    first = time.time() - t0
-    ms = []
-    for _ in range(3):
+
+
+
+def main():
+    names = sys.argv[2:] or list(worlds)
+    LIB = os.environ.get("VARIANT")  # a tools/build_variants.py variant instead of the main build
+    e = Engine(0, lib_path=os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build",
+                                        "variants", LIB, "libccka.so") if LIB else None)
+    import ctypes as C  # noqa: E402
+    e.lib.ccka_debug_engine.argtypes = [C.c_void_p, C.c_int32]
+    e.lib.ccka_debug_engine(e.ctx, 1)  # the general kernel for every world
+    ABL = [int(x) for x in os.environ.get("ABLATE", "0").split(",")]  # profiling: ccka_debug_ablate masks
+    e.lib.ccka_debug_ablate.argtypes = [C.c_void_p, C.c_int32]
+    for name, abl in [(n, a) for n in names for a in ABL]:
+        e.lib.ccka_debug_ablate(e.ctx, abl)
+        w = worlds[name]()
+        e.set_world(w)
+        e.set_scenarios(configs.hpa_scenarios(N))
+        e.gen_load(configs.trace_gen())
+        t0 = time.time()
         e.rollout(trajectory=False)
-        ms.append(e.kernel_ms())
-    eng = e.last_engine()[0]
-    m = sorted(ms)[1]
-    print(f"{name:20s} ablate={abl:2d} D={len(w.deploys):2d} slots={w.max_nodes:2d} engine={eng} kernel {m:9.2f} ms "
-          f"{N * w.n_steps / m * 1e3:.3e} cluster-steps/s (first call {first:.1f} s)", flush=True)
+        first = time.time() - t0
+        ms = []
+        for _ in range(3):
+            e.rollout(trajectory=False)
+            ms.append(e.kernel_ms())
+        eng = e.last_engine()[0]
+        m = sorted(ms)[1]
+        print(f"{name:20s} ablate={abl:2d} D={len(w.deploys):2d} slots={w.max_nodes:2d} engine={eng} kernel {m:9.2f} ms "
+              f"{N * w.n_steps / m * 1e3:.3e} cluster-steps/s (first call {first:.1f} s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
