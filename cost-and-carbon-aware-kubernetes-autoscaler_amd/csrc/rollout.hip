@@ -437,6 +437,9 @@ __device__ int behavior_long(const ccka_hpa_rules* up, const ccka_hpa_rules* dn,
 #ifndef MLP_W2PF
 #define MLP_W2PF 2
 #endif
+#ifndef MLP_BPF
+#define MLP_BPF 1
+#endif
 // ---- the learned policy inside the step loop (fused closed loop, POL > 0) ----
 // The MLP of mlp.hip (H1^T = W1^T X^T, H2^T = W2^T H1^T, Y^T = W3^T H2^T on
 // v_mfma_f32_32x32x16_bf16, each accumulator chained as the next layer's B
@@ -492,15 +495,19 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
   pbf16x8 wc[KS1], wn[KS1];
 #pragma unroll
   for (int s = 0; s < KS1; ++s) wc[s] = w1b0[s];
+  // the next block's bias tile (the accumulator's initial value) is read from
+  // LDS before this block's epilogue, which covers its latency (MLP_BPF)
+  pf32x16 cb = pbias_tile(s_b, h);
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
     if (n + 1 < NB) {
 #pragma unroll
       for (int s = 0; s < KS1; ++s) wn[s] = w1f[((n + 1) * KS1 + s) * 64 + lane];
     }
-    pf32x16 c = pbias_tile(s_b + 32 * n, h);
+    pf32x16 c = MLP_BPF ? cb : pbias_tile(s_b + 32 * n, h);
 #pragma unroll
     for (int s = 0; s < KS1; ++s) c = pmfma(wc[s], xf[s], c);
+    if (MLP_BPF) cb = pbias_tile(n + 1 < NB ? s_b + 32 * (n + 1) : s_b + MLP_HID, h);
     hh[2 * n] = prelu_pack(c, 0);
     hh[2 * n + 1] = prelu_pack(c, 1);
 #pragma unroll
@@ -518,7 +525,7 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
   for (int j = 0; j < PF; ++j) wq[j] = s_w2[j * 64 + lane];
 #pragma unroll
   for (int m = 0; m < NB; ++m) {
-    pf32x16 c = pbias_tile(s_b + MLP_HID + 32 * m, h);
+    pf32x16 c = MLP_BPF ? cb : pbias_tile(s_b + MLP_HID + 32 * m, h);
     const pbf16x8 w3a = s_w3[(2 * m) * 64 + lane], w3b = s_w3[(2 * m + 1) * 64 + lane];  // used after the chain
 #pragma unroll
     for (int kk = 0; kk < KS2; ++kk) {
@@ -527,6 +534,7 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
       if (nx < NB * KS2) wq[kk % PF] = s_w2[nx * 64 + lane];
       c = pmfma(w, hh[kk], c);
     }
+    if (MLP_BPF && m + 1 < NB) cb = pbias_tile(s_b + MLP_HID + 32 * (m + 1), h);
     y = pmfma(w3a, prelu_pack(c, 0), y);
     y = pmfma(w3b, prelu_pack(c, 1), y);
     __builtin_amdgcn_sched_barrier(0);
