@@ -545,6 +545,10 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
 #ifndef G_GATE_V
 #define G_GATE_V 1
 #endif
+// the several-deployment gate's sums reused by the candidate search (A/B macro)
+#ifndef DGATE_SEARCH_V
+#define DGATE_SEARCH_V 1
+#endif
 // v_permlane32_swap_b32: x's lanes 32..63 <-> y's lanes 0..31
 // (tools/probe/permlane.hip documents the lanes). Only for operands held in
 // separate scalars: ROCm 7.2 lowers a swap of two elements of one MFMA
@@ -1553,6 +1557,10 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       // pods; the budget and the PDB only restrict further); with none, the
       // evaluation would change nothing, so only the next wake step is kept.
       bool g_gate = true;
+      // several deployments: the gate's free-resource sums by capacity type
+      // (valid for the search below until its first deletion)
+      bool gsum = false;
+      int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;
       if constexpr (DMAX == 1) {
         if (G_GATE_V && g_eval && !gdrift && !greplace && !gmulti) {
           int F = 0;
@@ -1599,7 +1607,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
               pods += k;
             }
           };
-          int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;  // free resources by capacity type
+          gsum = true;  // free resources by capacity type
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) {
             if (!(rdy >> n & 1u)) continue;
@@ -2323,6 +2331,35 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
                 }
               }
             } else {
+              // the gate's necessary sums first (the state they were taken from
+              // until this evaluation's first deletion): a candidate they reject
+              // fails the first-fit trial below as well
+              if (DGATE_SEARCH_V && gsum && !any_deleted && bpods > 0) {
+                int c = 0, m = 0;
+                uint32_t cs = 0, xb = 0;
+#pragma unroll
+                for (int n = 0; n < MAXN; ++n)
+                  if (n == best) {
+                    xb = ninfo[n];
+#pragma unroll
+                    for (int e = 0; e < DMAX; ++e) {
+                      const int k = e < D ? npods[n][e] : 0;
+                      c += k * dep[e].req_cpu;
+                      m += k * dep[e].req_mem;
+                      cs |= k > 0 ? capsel[e] : 0u;
+                    }
+                  }
+                const bool s0 = (cs & capbit(0)) != 0, s1 = (cs & capbit(1)) != 0;
+                int vc = (s0 ? ac0 : 0) + (s1 ? ac1 : 0), vm = (s0 ? am0 : 0) + (s1 ? am1 : 0);
+                int vp = (s0 ? ap0 : 0) + (s1 ? ap1 : 0);
+                if (cs & capbit(ni_cap(xb))) {
+                  const ccka_itype& ty = L.types[ni_type(xb)];
+                  vc -= ty.alloc_cpu_m - c;
+                  vm -= ty.alloc_mem_mi - m;
+                  vp -= ty.max_pods - bpods;
+                }
+                if (!(c <= vc && m <= vm && bpods <= vp)) { rejected |= 1u << best; continue; }
+              }
               int tpods[MAXN][DMAX];
               int tlast[MAXN];
 #pragma unroll
