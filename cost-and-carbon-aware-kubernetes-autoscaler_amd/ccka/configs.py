@@ -63,6 +63,20 @@ def config2_world(n_steps: int = 1440, max_nodes: int = 8) -> WorldSpec:
                      n_steps=n_steps, max_nodes=max_nodes)
 
 
+def cheap_large_world(n_steps: int = 600, max_nodes: int = 8) -> WorldSpec:
+    """config 2 with every 4xlarge offering at 1/20 of its price: a claim of a
+    few pods launches a type far larger than it needs, so a launched node's pod
+    capacity (its type's) exceeds the claim's capacity bracket (regression
+    world for the argmin tables, SEMANTICS 3.F)."""
+    cat = catalog_small()
+    price = price_tiles(cat, 1, 3, SEED)
+    for k, name in enumerate(cat.names):
+        if name.endswith(".4xlarge"):
+            price[:, :, k] = np.maximum(price[:, :, k] // 20, 1)
+    return WorldSpec(catalog=cat, ci=carbon_intensity(1, SEED), price=price, pools=reference_pools(),
+                     deploys=[deployment(abi.SCALER_HPA)], n_steps=n_steps, max_nodes=max_nodes)
+
+
 def config3_world(n_steps: int = 1440, max_nodes: int = 8) -> WorldSpec:
     """8 regions x ~800-type catalog, Karpenter argmin with carbon weight."""
     cat = catalog_synth(800, SEED)

@@ -93,6 +93,7 @@ struct ccka_ctx {
   long long* d_acc = nullptr;
   int32_t* d_order = nullptr;
   int32_t* d_cap1s = nullptr;
+  int32_t* d_cap1t = nullptr;  // pod capacity per type (argmin-table entries)
   uint32_t* d_zmasks = nullptr;
   double* d_wc1000 = nullptr;
   uint8_t* d_wci = nullptr;
@@ -369,6 +370,7 @@ static int d1_check_world(ccka_ctx* c) {
   if ((rc = dupload(c, c->d_acc, acc.data(), acc.size())) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_order, order.data(), order.size())) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_cap1s, cap1s.data(), cap1s.size())) != CCKA_OK) return rc;
+  if ((rc = dupload(c, c->d_cap1t, cap1.data(), cap1.size())) != CCKA_OK) return rc;
   if ((rc = dupload(c, c->d_zmasks, zm.data(), zm.size())) != CCKA_OK) return rc;
   c->zmasks = zm;
   for (size_t z = 0; z < 16; ++z) p.zml[z] = z < zm.size() ? zm[z] : 0u;
@@ -616,7 +618,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_pswitch); dfree(c->d_cw); dfree(c->d_capsel); dfree(c->d_load); dfree(c->d_load_w); dfree(c->d_totals);
   dfree(c->d_ptable); dfree(c->d_pjtab); dfree(c->d_pwc);
   dfree(c->d_sinq);
-  dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_zmasks); dfree(c->d_wc1000);
+  dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_cap1t); dfree(c->d_zmasks); dfree(c->d_wc1000);
   dfree(c->d_wci); dfree(c->d_table); dfree(c->d_jtab); dfree(c->d_stamps);
   dfree(c->d_table2); dfree(c->d_jtab2); dfree(c->d_wc0);
   dfree(c->d_gstats); dfree(c->d_gcand); dfree(c->d_ggather); dfree(c->d_gcounts); dfree(c->d_gn);
@@ -1076,7 +1078,7 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     // single-deployment engine: argmin tables for this rollout, then the rollout
     TableParams tp{};
     tp.price = c->d_price; tp.ci_gpwh = c->d_ci_gpwh; tp.types = c->d_types;
-    tp.order = c->d_order; tp.cap1s = c->d_cap1s; tp.zmasks = c->d_zmasks; tp.wc1000 = c->d_wc1000;
+    tp.order = c->d_order; tp.cap1s = c->d_cap1s; tp.cap1t = c->d_cap1t; tp.zmasks = c->d_zmasks; tp.wc1000 = c->d_wc1000;
     tp.table = c->d_table; tp.jtab = c->d_jtab;
     tp.K = w.n_types; tp.Z = w.n_zones; tp.R = w.n_regions; tp.NZI = (int)c->zmasks.size();
     tp.NW = c->NW; tp.JT = c->JT;
@@ -1229,7 +1231,7 @@ static int policy_tables(ccka_ctx* c, KParams* k) {
   }
   TableParams tp{};
   tp.price = c->d_price; tp.ci_gpwh = c->d_ci_gpwh; tp.types = c->d_types;
-  tp.order = c->d_order; tp.cap1s = c->d_cap1s; tp.zmasks = c->d_zmasks; tp.wc1000 = c->d_pwc;
+  tp.order = c->d_order; tp.cap1s = c->d_cap1s; tp.cap1t = c->d_cap1t; tp.zmasks = c->d_zmasks; tp.wc1000 = c->d_pwc;
   tp.table = c->d_ptable; tp.jtab = c->d_pjtab;
   tp.K = w.n_types; tp.Z = w.n_zones; tp.R = w.n_regions; tp.NZI = (int)c->zmasks.size();
   tp.NW = NWP; tp.JT = c->JT;

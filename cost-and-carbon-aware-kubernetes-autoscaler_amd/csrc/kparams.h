@@ -261,6 +261,7 @@ struct TableParams {
   const ccka_itype* types;   // [K]
   const int32_t* order;      // [K] types by pod capacity desc, index asc
   const int32_t* cap1s;      // [K] pod capacity of order[i]
+  const int32_t* cap1t;      // [K] pod capacity of type k (the launched node's, SEMANTICS 3.E/F)
   const uint32_t* zmasks;    // [NZI]
   const double* wc1000;      // [NW] carbon weight * 1000
   int2* table;

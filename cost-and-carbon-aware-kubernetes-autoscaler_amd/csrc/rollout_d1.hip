@@ -142,7 +142,9 @@ __global__ void __launch_bounds__(256) table_kernel(TableParams q) {
       // spot first when any spot offering holds n (the F launch rule); the
       // G2 offer rule takes the cheapest of all
       const Best& w = (!q.offer && bs.info >= 0) ? bs : ba;
-      const int info = w.info >= 0 ? (w.info | c1 << 16) : -1;
+      // the node's pod capacity is its type's, which may exceed the bracket's
+      // c1 when a larger type wins the claim
+      const int info = w.info >= 0 ? (w.info | q.cap1t[w.k] << 16) : -1;
       const int hi = min(c1, q.JT - 1);
       for (int n = c1n + 1; n <= hi; ++n) out[n] = make_int2(w.price, info);
     }

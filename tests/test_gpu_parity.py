@@ -71,6 +71,26 @@ def test_config3_catalog800_regions(engine):
     compare(rg, rc, tg, tc)
 
 
+def test_larger_type_wins_small_claim(engine):
+    """A claim of a few pods won by a much larger type: the launched node holds
+    its type's pod capacity, not the claim's capacity bracket (the argmin
+    tables carry the winner's capacity). Both engines against the oracle."""
+    spec = configs.cheap_large_world()
+    sc = configs.hpa_scenarios(2000)
+    load = po.gen_load(configs.trace_gen(), spec.n_steps, 1, sc.n)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    kinds = set((rc["last_choice"] & 0xFFF).tolist())
+    assert kinds and kinds <= {3, 7, 11, 15}  # only 4xlarge types launch
+    for mode in (0, 1):  # automatic (single-deployment engine), general kernel
+        engine.set_engine(mode)
+        try:
+            rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+            assert engine.last_engine()[0] == (2 if mode == 0 else 1)
+        finally:
+            engine.set_engine(0)
+        compare(rg, rc, tg, tc)
+
+
 def test_config1_replay_12_deployments(engine):
     spec = configs.config1_world()
     sc = ScenarioSet(1)

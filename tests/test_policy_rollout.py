@@ -15,8 +15,8 @@ from parity import compare
 THREADS = 16
 
 
-def _case(n=512, T=180, drift=0):
-    spec = configs.config2_world(n_steps=T)
+def _case(n=512, T=180, drift=0, world=None):
+    spec = (world or configs.config2_world)(n_steps=T)
     spec.drift = drift
     sc = configs.hpa_scenarios(n, first_id=99)
     load = po.gen_load(configs.trace_gen(5), T, 1, n, first_id=99)
@@ -49,11 +49,14 @@ def test_oracle_replay_matches_fixed_overrides():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("drift", [0, 1])
+@pytest.mark.parametrize("drift", [0, 1, "cheap_large"])
 def test_closed_loop_policy_parity(engine, drift):
     import torch
     from test_gpu_mlp import torch_ref
-    spec, sc, load = _case(drift=drift)
+    if drift == "cheap_large":  # table launches of a type larger than the claim (SEMANTICS 3.F)
+        spec, sc, load = _case(world=configs.cheap_large_world)
+    else:
+        spec, sc, load = _case(drift=drift)
     ws, bs = configs.mlp_weights(11)
     wb = [configs.to_bf16_bits(w) for w in ws]
     engine.set_world(spec)
