@@ -281,6 +281,22 @@ class Engine:
         self.lib.ccka_debug_engine.argtypes = [C.c_void_p, C.c_int32]
         self._chk(self.lib.ccka_debug_engine(self.ctx, mode), "ccka_debug_engine")
 
+    def debug_pool(self, mode: int = -1, min_queue: int = 0) -> int:
+        """Internal: pooled event steps of the single-deployment engine (1 on,
+        0 off, -1 unchanged) and the queue length at which a wave serves the
+        queue (0 unchanged); returns whether the last such rollout was pooled."""
+        fn = self.lib.ccka_debug_pool
+        fn.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]
+        last = C.c_int32(0)
+        self._chk(fn(self.ctx, mode, min_queue, C.byref(last)), "ccka_debug_pool")
+        return last.value
+
+    def debug_pool_policy(self, age: int, idle: int = 1):
+        """Internal: the pooled kernel's other serving rules (see ccka_abi.cpp)."""
+        fn = self.lib.ccka_debug_pool_policy
+        fn.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        self._chk(fn(self.ctx, age, idle), "ccka_debug_pool_policy")
+
     def last_engine(self):
         """Internal: (engine, table_ms) of the last rollout; engine 1 = general
         kernel, 2 = single-deployment kernel (rollout_d1.hip)."""

@@ -107,6 +107,11 @@ struct ccka_ctx {
   unsigned long long* d_stamps = nullptr;
   int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
   int occ = 0;               // its register-allocation occupancy target (0 = automatic)
+  int pool_mode = 0;         // 1: pooled event steps (rollout_pool.hip, an A/B engine: measured slower) where eligible
+  int pool_min = 48;         // queue length at which a wave serves it
+  int pool_age = 20000;      // or any waiting entries once the last claim is this many cycles old
+  int pool_idle = 1;         // or any waiting entries when none of its own lanes can step
+  bool last_pooled = false;  // the last single-deployment rollout ran the pooled kernel
   int mlp_stamps = 0;        // diagnostic MLP phase stamps (ccka_debug_mlp_stamps)
   // policy sweep (config 4)
   ccka_grid_stats* d_gstats = nullptr;   // [grids] then [2 * grids] scratch
@@ -832,6 +837,27 @@ static int ensure_load(ccka_ctx* c) {
   return CCKA_OK;
 }
 
+// The pooled single-deployment kernel (rollout_pool.hip) takes the worlds with
+// the default HPA behavior or one KEDA trigger, one decision per step, <= 8
+// slots and <= 2 pools, no drift / replacement / multi-node consolidation,
+// when the workgroup's scenario state fits the 160 KiB of LDS (price tiles
+// staged too when they fit) and its trace resource spans < 2 GiB; the others
+// keep rollout_d1_kernel.
+static bool d1_pool_plan(const ccka_ctx* c, D1Params& p) {
+  if (!c->pool_mode || !p.bdef || p.nsub != 1 || p.drift || p.maxn > 8 || p.NP > 2 || (p.ablate & ~16) ||
+      (p.stamps && p.keda) || c->occ > 2 || p.lpw < 1 || p.lpw > 64)
+    return false;
+  if (!p.load_w && p.NL * (int64_t)p.T * 4 >= (1LL << 31)) return false;
+  const int hw = p.he4 ? 2 : 4;
+  for (int tab = 1; tab >= 0; --tab) {
+    if (pool_lds_layout(p.K, p.R, p.Z, p.NZI, tab, PL_WAVES * p.lpw, hw).total <= 160u * 1024u) {
+      p.lds_tab = tab;
+      return true;
+    }
+  }
+  return false;
+}
+
 // scenarios per wave of the single-deployment kernel: a wave's cost is the
 // union of its lanes' event paths, so when the batch is smaller than one full
 // round of resident waves (two per SIMD at this kernel's register budget)
@@ -854,7 +880,7 @@ static int d1_trace_tile(ccka_ctx* c) {
   if (!c->d1_world || c->hw.n_deploy != 1 || c->n_traces > 0 || !c->have_load) return CCKA_OK;
   const int32_t lpw = d1_lpw(c);
   if (c->load_w_lpw == lpw && c->d_load_w) return CCKA_OK;
-  const int64_t cnt = (int64_t)c->hw.n_steps * c->N;
+  const int64_t cnt = (int64_t)c->hw.n_steps * ((c->N + lpw - 1) / lpw * lpw);  // rows lpw wide
   if (!c->d_load_w || c->load_w_count != cnt) {
     dfree(c->d_load_w);
     c->load_w_count = 0;
@@ -1125,7 +1151,14 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
       p.table2 = c->d_table2;
     }
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
-    HIPCHK(c, launch_rollout_d1(p, c->stream));
+    p.cap1t = c->d_cap1t;
+    p.pool_min = c->pool_min;
+    p.pool_age = c->pool_age;
+    p.pool_idle = c->pool_idle;
+    D1Params q = p;
+    c->last_pooled = d1_pool_plan(c, q);
+    if (c->last_pooled) HIPCHK(c, launch_rollout_pool(q, c->stream));
+    else HIPCHK(c, launch_rollout_d1(p, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_engine = 2;
     c->traj_nt = true;
@@ -2397,6 +2430,28 @@ int ccka_debug_lpw(ccka_ctx* c, int32_t lpw) {
 int ccka_debug_trace_flat(ccka_ctx* c, int32_t on) {
   if (!c) return CCKA_EINVAL;
   c->trace_flat = on != 0;
+  return CCKA_OK;
+}
+
+// Internal: pooled event steps of the single-deployment engine (mode 1; 0 =
+// rollout_d1_kernel everywhere, the default: DESIGN.md "Pooled event steps,
+// built and measured") and the queue length at which a
+// wave serves the queue (1..64; 0 = the default 48); `last` (nullable): whether
+// the last single-deployment rollout ran the pooled kernel.
+int ccka_debug_pool(ccka_ctx* c, int32_t mode, int32_t min_queue, int32_t* last) {
+  if (!c || mode < -1 || mode > 1 || min_queue < 0 || min_queue > 64) return CCKA_EINVAL;
+  if (mode >= 0) c->pool_mode = mode;
+  if (min_queue > 0) c->pool_min = min_queue;
+  if (last) *last = c->last_pooled ? 1 : 0;
+  return CCKA_OK;
+}
+
+// Internal: the other serving rules of the pooled kernel (age in s_memtime
+// cycles since the last claim, >= 0; idle: serve when no own lane can step).
+int ccka_debug_pool_policy(ccka_ctx* c, int32_t age, int32_t idle) {
+  if (!c || age < 0 || idle < 0 || idle > 1) return CCKA_EINVAL;
+  c->pool_age = age;
+  c->pool_idle = idle;
   return CCKA_OK;
 }
 

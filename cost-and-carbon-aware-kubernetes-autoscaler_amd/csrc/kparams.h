@@ -252,7 +252,21 @@ struct D1Params {
   int32_t k_cds;   // cooldownPeriod in whole steps: ceil(cooldown_s / 60), >= 0
   int32_t k_min;   // minReplicaCount
   int32_t k_max;   // maxReplicaCount
+  // pooled event steps (rollout_pool.hip)
+  const int32_t* cap1t;  // [K] pod capacity per type (the slots' capacity is their type's)
+  int32_t pool_min;      // a wave serves the queue once it holds this many scenarios,
+  int32_t pool_age;      // or any once the last claim is this many cycles old,
+  int32_t pool_idle;     // or any when none of its own lanes can step (1)
+  int32_t _ppad;
 };
+
+// rollout_pool_kernel: one 8-wave workgroup per CU, the scenario state in LDS
+constexpr int PL_WAVES = 8;
+struct PoolLds {
+  uint32_t cap1, tab, win, queue, rqueue, ctrl, state, total;  // byte offsets into the dynamic LDS, total size
+};
+__host__ __device__ PoolLds pool_lds_layout(int K, int R, int Z, int NZI, int lds_tab, int sb, int hw);
+hipError_t launch_rollout_pool(const D1Params& p, hipStream_t s);
 
 // argmin-table builder: one wave per (region, hour, zone-mask, cap-mask, carbon weight)
 struct TableParams {

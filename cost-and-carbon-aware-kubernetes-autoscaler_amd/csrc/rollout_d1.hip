@@ -901,7 +901,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
   }();
   const int32_t* lp = p.load_w ? p.load_w + wtb * T + lane
                                : p.load + (p.trace_mod > 0 ? (p.first_id + i) % p.trace_mod : i);
-  const long long lsl = opq(p.load_w ? (long long)min((int64_t)p.lpw, p.N - wtb) : (long long)p.NL);
+  const long long lsl = opq(p.load_w ? (long long)p.lpw : (long long)p.NL);  // tiled rows: lpw wide (the last wave padded)
   // load-sample ring of this wave
   const uint32_t ring_off = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(((uint32_t)p.K * 16u + 255u) / 256u * 256u + (threadIdx.x / WAVE) * (uint32_t)D1_RING_BYTES));
@@ -2156,17 +2156,17 @@ hipError_t launch_traj_transpose(const ccka_traj_rec* in, ccka_traj_rec* out, in
   return hipGetLastError();
 }
 
-// [T][N] load trace -> wave-tiled [wave][T][lanes] (the single-deployment
-// kernel's read layout: a wave's rows contiguous, lanes = lpw but the last
-// wave's remainder), once per trace / lanes-per-wave change (ccka_abi.cpp
-// d1_trace_tile); reads coalesced, writes in runs of `lanes` ints.
+// [T][N] load trace -> wave-tiled [wave][T][lpw] (the single-deployment
+// kernels' read layout: a wave's rows contiguous, every row lpw wide, the last
+// wave's padded: one row stride for all), once per trace / lanes-per-wave
+// change (ccka_abi.cpp d1_trace_tile); reads coalesced, writes in runs of lpw ints.
 __global__ void __launch_bounds__(256) trace_tile_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
                                                          int64_t N, int64_t T, int64_t lpw) {
   const int64_t total = N * T, stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += stride) {
     const int64_t t = x / N, n = x - t * N;
-    const int64_t w0 = n / lpw * lpw, wl = min(lpw, N - w0);
-    out[w0 * T + t * wl + (n - w0)] = in[x];
+    const int64_t w0 = n / lpw * lpw;
+    out[w0 * T + t * lpw + (n - w0)] = in[x];
   }
 }
 
