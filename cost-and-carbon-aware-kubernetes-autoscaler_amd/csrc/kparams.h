@@ -26,6 +26,16 @@ __host__ __device__ constexpr int64_t state_words(int dmax, int nmax) {
 constexpr int MLP_IN = 64, MLP_HID = 256, MLP_OUT = 8;
 typedef short mlp_bf16x8 __attribute__((ext_vector_type(8)));
 
+// Profiling-only phase switches (ccka_debug_ablate bits 1/2/4/8/32: skip
+// disruption / provisioning / the detail breakdown / the HPA behavior / the
+// fused loop's MLP). Compiled in only by variant builds
+// (tools/build_variants.py name=-DCCKA_ABLATE_BUILD=1, tools/ablate.py); the
+// shipping kernels fold every switch away.
+#ifndef CCKA_ABLATE_BUILD
+#define CCKA_ABLATE_BUILD 0
+#endif
+__host__ __device__ constexpr bool ablated(int mask, int bits) { return CCKA_ABLATE_BUILD && (mask & bits) != 0; }
+
 struct KParams {
   const ccka_world* w;  // device copy (pools, deployments, scalars)
   const ccka_itype* types;

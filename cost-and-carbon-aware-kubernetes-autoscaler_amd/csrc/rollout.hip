@@ -541,14 +541,6 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
   }
   return y;
 }
-// the exact disruption gate of one-deployment worlds (0: the A/B variant)
-#ifndef G_GATE_V
-#define G_GATE_V 1
-#endif
-// the several-deployment gate's sums reused by the candidate search (A/B macro)
-#ifndef DGATE_SEARCH_V
-#define DGATE_SEARCH_V 1
-#endif
 // v_permlane32_swap_b32: x's lanes 32..63 <-> y's lanes 0..31
 // (tools/probe/permlane.hip documents the lanes). Only for operands held in
 // separate scalars: ROCm 7.2 lowers a swap of two elements of one MFMA
@@ -976,7 +968,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       const int hl = lane >> 5;
       GK_STAMP(7);  // features, X^T operands
       pf32x16 ya, yb;
-      if (p.ablate & 32) {  // profiling only: the loop without its MLP
+      if (ablated(p.ablate, 32)) {  // profiling only: the loop without its MLP
 #pragma unroll
         for (int k = 0; k < 16; ++k) ya[k] = yb[k] = 0.f;
       } else {
@@ -1219,13 +1211,13 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
             }
           }
         }
-        if (do_behavior && !(p.ablate & 8) && p.hlen) {
+        if (do_behavior && !ablated(p.ablate, 8) && p.hlen) {
           ran = true;
           const ccka_deployment& gd = gw->deploy[d];
           const int dstab = p.down_stab && dp.scaler == CCKA_SCALER_HPA ? (int)p.down_stab[i] : gd.down.stab_window_s;
           desired = behavior_long(&gd.up, &gd.down, dstab, p.sync_s, cur, proposal, minr, mx, p.hist + (int64_t)d * p.N + i,
                                   hpos, p.hlen, (int64_t)D * p.N);
-        } else if (do_behavior && !(p.ablate & 8)) {
+        } else if (do_behavior && !ablated(p.ablate, 8)) {
           ran = true;
           // stabilisation over the valid records inside each window
           const uint32_t upm = recv[d] & (uint32_t)dp.up.stab_mask;
@@ -1348,7 +1340,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       // wave-cooperative scans below, lane-local (rollout_d1_kernel's F2)
       uint32_t fm = ~used & slot_mask;
       int pd = pend[0];
-      if (active && pd > 0 && fm && !(p.ablate & 2)) {
+      if (active && pd > 0 && fm && !ablated(p.ablate, 2)) {
         const int rh = my_r * 24 + hour;
         int q = -1, J = 0, zi = 0;
         uint32_t cm = 0;
@@ -1404,7 +1396,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) anyp |= pend[d] > 0;
       const uint32_t free_mask = ~used & slot_mask;
-      unsigned long long need = __ballot(active && anyp && free_mask != 0 && !(p.ablate & 2));
+      unsigned long long need = __ballot(active && anyp && free_mask != 0 && !ablated(p.ablate, 2));
       while (need) {
         const int ld = __ffsll((long long)need) - 1;
         need &= need - 1;
@@ -1548,7 +1540,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     GK_STAMP(4);  // provisioning
     if (active) {
       // ---- G. disruption (skipped exactly when nothing it depends on moved) ----
-      const bool g_eval = (g_dirty || t >= g_wake) && !(p.ablate & 1);
+      const bool g_eval = (g_dirty || t >= g_wake) && !ablated(p.ablate, 1);
       // One deployment without drift / replacement / multi-node consolidation:
       // an exact gate first (the single-deployment kernel's). The phase acts
       // only on a ready candidate past its consolidateAfter that is empty, or
@@ -1562,7 +1554,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       bool gsum = false;
       int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;
       if constexpr (DMAX == 1) {
-        if (G_GATE_V && g_eval && !gdrift && !greplace && !gmulti) {
+        if (g_eval && !gdrift && !greplace && !gmulti) {
           int F = 0;
           uint32_t cm1 = 0, el = 0;
 #pragma unroll
@@ -1596,7 +1588,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         // pod count must fit those nodes' free resources (the candidate's own
         // excluded); with no candidate that is empty or passes these sums, the
         // sequential search would reject every one.
-        if (G_GATE_V && g_eval && !gdrift && !greplace && !gmulti) {
+        if (g_eval && !gdrift && !greplace && !gmulti) {
           auto node_use = [&](int n, int& c, int& m, int& pods) {
             c = 0; m = 0; pods = 0;
 #pragma unroll
@@ -2334,7 +2326,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
               // the gate's necessary sums first (the state they were taken from
               // until this evaluation's first deletion): a candidate they reject
               // fails the first-fit trial below as well
-              if (DGATE_SEARCH_V && gsum && !any_deleted && bpods > 0) {
+              if (gsum && !any_deleted && bpods > 0) {
                 int c = 0, m = 0;
                 uint32_t cs = 0, xb = 0;
 #pragma unroll
@@ -2475,7 +2467,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       long long e_step = base_nw;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        if (!(used >> n & 1u) || (p.ablate & 4)) continue;
+        if (!(used >> n & 1u) || ablated(p.ablate, 4)) continue;
         const ccka_itype& ty = L.types[ni_type(ninfo[n])];
         long long use = 0;
         if (rdy >> n & 1u) {

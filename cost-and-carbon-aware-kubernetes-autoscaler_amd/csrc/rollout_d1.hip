@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "../../include/ccka.h"
+#include "d1_common.h"
 #include "kparams.h"
 
 #pragma clang fp contract(off)
@@ -36,10 +37,6 @@
 namespace ccka {
 
 namespace {
-
-constexpr int WAVE = 64;
-
-__device__ __forceinline__ int capbit1(int c) { return c == 0 ? CCKA_CAP_SPOT : CCKA_CAP_OD; }
 
 // ---------------------------------------------------------------------------
 // argmin tables
@@ -164,23 +161,6 @@ namespace {
 // ---------------------------------------------------------------------------
 // rollout helpers
 // ---------------------------------------------------------------------------
-// Opaque copy of a kernel argument: the value then lives in a register for the
-// whole loop (spilled to a VGPR lane if need be) instead of being re-read from
-// the kernarg segment with an s_load + lgkmcnt wait at each use.
-template <class V>
-__device__ __forceinline__ V opq(V v) {
-  asm volatile("" : "+s"(v));
-  return v;
-}
-// global-memory pointer made opaque the same way, keeping its address space
-// (a generic pointer would turn every access into a flat_* instruction)
-#define GLOBAL_AS __attribute__((address_space(1)))
-template <class V>
-__device__ __forceinline__ GLOBAL_AS V* opq_ptr(V* v) {
-  uint64_t x = (uint64_t)v;
-  asm volatile("" : "+s"(x));
-  return (GLOBAL_AS V*)x;
-}
 // per-lane variant: the value is redefined by the asm, so no load is pending
 // on it afterwards (the wait for the load happens here, not at its next use)
 __device__ __forceinline__ int opqv(int v) {
@@ -207,48 +187,6 @@ __device__ __forceinline__ D1Rule opq_rule(const D1Rule& r) {
     o.pm16[1][w] = opq(r.pm16[1][w]);
   }
   return o;
-}
-
-__device__ __forceinline__ int wmask(int window_s) {
-  int m = 0;
-#pragma unroll
-  for (int k = 0; k < CCKA_HIST; ++k) m |= ((k + 1) * CCKA_STEP_SECONDS < window_s) ? (1 << k) : 0;
-  return m;
-}
-
-// packed int16 history rings: entry k (k steps old, 0 = this step) sits in
-// half k&1 of word k>>1
-template <int W = 4>
-__device__ __forceinline__ void ring_push(uint32_t* r, int v) {
-#pragma unroll
-  for (int w = W - 1; w > 0; --w) r[w] = __builtin_amdgcn_alignbit(r[w], r[w - 1], 16);
-  r[0] = (r[0] << 16) | ((uint32_t)v & 0xFFFFu);
-}
-// four equal records at once (one step of 15 s decisions): a two-word shift
-template <int W>
-__device__ __forceinline__ void ring_push4(uint32_t* r, int v) {
-#pragma unroll
-  for (int w = W - 1; w > 1; --w) r[w] = r[w - 2];
-  r[1] = r[0] = ((uint32_t)v & 0xFFFFu) * 0x10001u;
-}
-
-typedef short short2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ short2v as_s2(uint32_t x) { return __builtin_bit_cast(short2v, x); }
-// (m & a) | (~m & b): v_bfi_b32
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-
-// floor(a / b) for 0 <= a < 2^31, 1 <= b < 2^30, given rb = 1/(float)b
-// (v_rcp_f32), without a branch: the f32 estimate is within one of the
-// quotient while the quotient is below 2^20, and one remainder test corrects
-// it. `bad` is set when those preconditions fail (the caller then recomputes
-// exactly); lanes whose inputs are meaningless get a meaningless quotient and
-// no fault.
-__device__ __forceinline__ int fdiv_nb(int a, int b, float rb, bool& bad) {
-  int q = (int)((float)a * rb);
-  const int r = (int)((uint32_t)a - (uint32_t)q * (uint32_t)b);
-  q += (r >= b ? 1 : 0) - (r < 0 ? 1 : 0);
-  bad = bad || (uint32_t)q >= (1u << 20) || (uint32_t)b >= (1u << 30);
-  return q;
 }
 
 // convertDesiredReplicasWithBehaviorRate, one direction. The period sums of
@@ -332,20 +270,11 @@ static_assert(D1_VMN + 4 * D1_S + D1_BACK <= D1_RB && D1_RB - D1_S - D1_BACK - D
               "ring too small for the DMA lead");
 constexpr int D1_RING_BYTES = D1_RB * WAVE * 4;  // per wave
 // Trajectory records go through a buffer resource over the wave's [lanes][T]
-// record block: the hardware drops a store whose offset lies past num_records,
-// so an out-of-range offset masks a lane's store without an exec-mask branch,
-// and num_records = 0 turns every store off when no trajectory is kept.
-constexpr int D1_NOSTORE = 0x7FFFFFF0;
+// record block (d1_store_rec, d1_common.h).
 // wave priority raised outside the event runs (quiet steps and the loop): 4 %
 // faster than none in round 3, whatever the level and direction (the gain is
 // as much the s_setprio boundaries as the arbitration)
 constexpr int D1_PRIO_HI = 3;
-__device__ __forceinline__ void d1_store_rec(__amdgpu_buffer_rsrc_t r, int voff, const int4& v) {
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, voff, 0, 0);
-}
-
 __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row) {
   unsigned keep;
   asm volatile(
@@ -360,42 +289,6 @@ __device__ __forceinline__ void d1_dma_row(const int32_t* src, uint32_t lds_row)
 }
 __device__ __forceinline__ void d1_wait_rows() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D1_VMN) : "memory"); }
 __device__ __forceinline__ void d1_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Argmin-table reads of the event step through the scalar data cache: a
-// vector load would wait for every older vector-memory operation of the wave
-// (the last iteration's trajectory stores and trace DMAs: they complete in
-// issue order), a scalar load only for older scalar ones. The active lanes'
-// addresses are taken four at a time (v_readlane), loaded with s_load_dwordx2
-// and handed back to their lanes.
-#define CONST_AS __attribute__((address_space(4)))
-__device__ __forceinline__ int2 d1_tload(const GLOBAL_AS int2* ptr) {
-  const uint64_t a = (uint64_t)ptr;
-  const int alo = (int)(uint32_t)a, ahi = (int)(uint32_t)(a >> 32);
-  const int me = (int)(threadIdx.x & (WAVE - 1));
-  uint64_t m = __ballot(1);
-  int ox = 0, oy = 0;
-  while (m) {
-    int l[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      l[k] = m ? __ffsll((long long)m) - 1 : l[0];
-      m &= m - 1;  // (0 stays 0)
-    }
-    uint64_t v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint64_t ak = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(alo, l[k]) |
-                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane(ahi, l[k]) << 32;
-      v[k] = *(const CONST_AS uint64_t*)ak;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      ox = me == l[k] ? (int)(uint32_t)v[k] : ox;
-      oy = me == l[k] ? (int)(uint32_t)(v[k] >> 32) : oy;
-    }
-  }
-  return make_int2(ox, oy);
-}
 
 // logical block of dispatch block b among n (a bijection; 8 XCDs)
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
@@ -489,7 +382,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
 
   // ---- kernel arguments used inside the step loop (opaque register copies) ----
   const int NP = opq(p.NP), NZI = opq(p.NZI), NW = opq(p.NW), JT = opq(p.JT);
-  const int maxn = opq(p.maxn), ablate = opq(p.ablate), pdb_member = opq(p.pdb_member);
+  const int maxn = opq(p.maxn), ablate = CCKA_ABLATE_BUILD ? opq(p.ablate) : 0, pdb_member = opq(p.pdb_member);
   const int pdb_pct = opq(p.pdb_pct), slo_util = opq(p.slo_util), delay = opq(p.delay);
   const int base_nodes = opq(p.base_nodes), base_type = opq(p.base_type);
   const int K = opq(p.K), Z = opq(p.Z), T = opq(p.T);
@@ -782,7 +675,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
     o.ran = metric;
     o.hpa_path = !(cur == 0 && minr != 0);
     int desired = cur > mx ? mx : (cur < minr && o.hpa_path ? minr : cur);
-    if (metric && !(ablate & 8)) desired = behave(proposal, cur);
+    if (metric && !ablated(ablate, 8)) desired = behave(proposal, cur);
     o.desired = desired;
     return o;
   };
@@ -821,7 +714,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         }
         o.proposal = prop;
         o.ran = true;
-        desired = (ablate & 8) ? cur : behave(prop, cur);
+        desired = ablated(ablate, 8) ? cur : behave(prop, cur);
       }
     }
     o.desired = desired;
@@ -1218,7 +1111,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // ---- F2. Karpenter provisioning: claims of min(J, pending) pods ----
         {
           uint32_t fm = ~used & slot_mask;
-          if (pd > 0 && fm && !(ablate & 2)) {
+          if (pd > 0 && fm && !ablated(ablate, 2)) {
             int q = -1, J = 0, zq = 0, cq = 0;
             uint32_t cm = 0;
 #pragma unroll
@@ -1312,7 +1205,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
         // being replaced are drift candidates (G0)
         const uint32_t tkm = DRIFT ? (repm & rdy) : 0u;
         const uint32_t dwork = DRIFT ? (dmask & rdy & ~srcm) : 0u;
-        if ((gate || tkm || dwork) && !(ablate & 1)) {
+        if ((gate || tkm || dwork) && !ablated(ablate, 1)) {
           bool any_del = false;
           // free capacity of the compatible ready untainted slots, from scratch
           auto ffree_now = [&]() {
@@ -1992,7 +1885,7 @@ __global__ void __launch_bounds__(256, OCC) rollout_d1_kernel(D1Params p) {
                                      ((DRIFT && G3 && multi) ? (weou_e & ~emp_e & ~taint()) : 0u));
 #pragma unroll
           for (int n = 0; n < MAXN; ++n) nx = ((gm >> n & 1u) && slc[n] > t) ? min(nx, slc[n]) : nx;
-          if (g_acted || (ablate & 15)) nx = t + 1;  // ablation runs: every step an event
+          if (g_acted || ablated(ablate, 15)) nx = t + 1;  // ablation runs: every step an event
           nxt = nx;
         }
       }
