@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--deployments", type=int, default=1,
                     help="config 2 with this many HPA deployments sharing each cluster's nodes (the general "
                          "kernel's multi-deployment layouts; 8 node slots up to 2 deployments, else 16)")
+    ap.add_argument("--mlp-tile", type=int, choices=(16, 32), default=16,
+                    help="config 5 forward: mlp16_kernel (16x16x32 MFMA, default) or mlp_kernel (32x32x16)")
     ap.add_argument("--keda", action="store_true",
                     help="configs 2-3 with a KEDA ScaledObject queue worker instead of the HPA deployment "
                          "(SURVEY A.2 defaults: scale from / to zero, cooldown 300 s, min 0, max 100; threshold "
@@ -84,6 +86,8 @@ def main():
     ap.add_argument("--spawn", action="store_true",
                     help="run the ranks as fresh child processes even at --gpus 1 (the launcher path)")
     args = ap.parse_args()
+    if args.deployments > 1 and (args.config != 2 or args.keda):
+        ap.error("--deployments applies to config 2 with HPA deployments only (not with --keda)")
 
     # one process per GPU: without a launcher's rank environment, this process
     # only starts the N rank processes (it never touches a GPU itself)
@@ -169,6 +173,9 @@ def main():
         ws, bs = configs.mlp_weights(11)
         eng.mlp_set_weights([configs.to_bf16_bits(w) for w in ws], bs)
         eng.mlp_gen_states(N, seed=7 + rank)
+        mt = eng.lib.ccka_debug_mlp_tile
+        mt.argtypes = [C.c_void_p, C.c_int32]
+        eng._chk(mt(eng.ctx, args.mlp_tile), "ccka_debug_mlp_tile")
         step_fn = eng.mlp_forward_async
         traj = False
     else:
@@ -310,7 +317,7 @@ def main():
                        "states_per_gpu": N, "parallelism": f"data-parallel x{world}"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_DENSE_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
-                         "kernel": "mlp_kernel", "kernel_ms_avg": avg_ms,
+                         "kernel": "mlp16_kernel" if args.mlp_tile == 16 else "mlp_kernel", "kernel_ms_avg": avg_ms,
                          "flops_per_launch": flops},
         }
         if rank == 0 and world == 1 and not args.no_cpu:

@@ -184,6 +184,22 @@ def test_spot_first_even_if_od_cheaper():
     assert ((r["last_choice"][0] >> 14) & 3) == 0  # still spot
 
 
+def test_claim_skips_a_pool_its_limits_exhaust():
+    """SEMANTICS 3.F: new claims go to the first pool (Karpenter order) that
+    admits the pods' capacity types AND can hold one of them under its limits
+    (found by the independent restatement, tests/spec_model.py: Karpenter then
+    tries the next NodePool). on-demand-slo comes first for selector-less pods;
+    with its CPU limit at 0 every claim lands in spot-preferred instead."""
+    dep = [deployment(abi.SCALER_STATIC, replicas0=4, min_r=4, max_r=4, cap_sel=abi.CAP_SPOT | abi.CAP_OD)]
+    spec = tiny_world(dep, T=3, peak_switch=0)
+    r, _ = run(spec, np.zeros((3, 1, 1), np.int32))
+    assert r["last_choice"][0] >> 16 == 0  # unlimited: the on-demand pool
+    spec.pools[0].limit_cpu_m = 0
+    r, tr = run(spec, np.zeros((3, 1, 1), np.int32))
+    assert r["launches"][0] >= 1 and r["last_choice"][0] >> 16 == 1  # the spot pool
+    assert tr["pending"][1, 0] == 0
+
+
 def test_keda_scale_to_zero_and_when_empty_timing():
     """KEDA: active for 10 steps then idle. Scale 1->0 after the 300 s cooldown
     (5 steps after the last active step), node then empty; WhenEmpty/30 s in
