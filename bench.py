@@ -62,7 +62,11 @@ def main():
                          "WhenEmptyOrUnderutilized pools)")
     ap.add_argument("--deployments", type=int, default=1,
                     help="config 2 with this many HPA deployments sharing each cluster's nodes (the general "
-                         "kernel's multi-deployment layouts; 8 node slots up to 2 deployments, else 16)")
+                         "kernel's multi-deployment layouts; 8 node slots up to 2 deployments, else 16; from 5 on "
+                         "the demo_30 burst shape: alternating spot / on-demand deployments of 5 replicas, "
+                         "max 10 each, no per-scenario overrides)")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="--deployments: the general kernel in lockstep instead of its lane-skewed schedule (A/B)")
     ap.add_argument("--mlp-tile", type=int, choices=(16, 32), default=16,
                     help="config 5 forward: mlp16_kernel (16x16x32 MFMA, default) or mlp_kernel (32x32x16)")
     ap.add_argument("--keda", action="store_true",
@@ -201,9 +205,20 @@ def main():
             gen = configs.config4_trace_gen()
             traj = (args.mode or "summary") == "trajectory"
         if args.deployments > 1:  # several HPA deployments per cluster (demo_30's burst shape)
-            spec.deploys = [configs.deployment(abi.SCALER_HPA, replicas0=3, max_r=30,
-                                               req_cpu=(200, 300, 250, 400)[d % 4], target=(70, 60, 80, 50)[d % 4])
-                            for d in range(args.deployments)]
+            if args.deployments <= 4:
+                spec.deploys = [configs.deployment(abi.SCALER_HPA, replicas0=3, max_r=30,
+                                                   req_cpu=(200, 300, 250, 400)[d % 4], target=(70, 60, 80, 50)[d % 4])
+                                for d in range(args.deployments)]
+            else:
+                # demo_30_burst_configure.sh:57-151: odd (1-based) deployments select spot, even
+                # on-demand, 5 replicas each; each keeps its own capacity type and bounds
+                spec.deploys = [configs.deployment(abi.SCALER_HPA, replicas0=5, max_r=10,
+                                                   cap_sel=abi.CAP_SPOT if d % 2 == 0 else abi.CAP_OD,
+                                                   req_cpu=(200, 300, 250, 400)[d % 4], target=(70, 60, 80, 50)[d % 4])
+                                for d in range(args.deployments)]
+                sc.cap_sel = None
+                sc.max_replicas = None
+                sc.target_util_pct = None
             spec.max_nodes = 8 if args.deployments <= 2 else 16
         if args.keda:  # the queue-worker side of the path: one ScaledObject per scenario
             spec.deploys = [configs.deployment(abi.SCALER_KEDA, replicas0=0, keda_threshold=500, keda_activation=0,
@@ -217,6 +232,8 @@ def main():
                 pool.budget_pct = args.budget
         eng.set_world(spec)
         eng.set_scenarios(sc)
+        if args.lockstep:
+            eng.set_engine(2)
         if args.trace_flat:
             tf = eng.lib.ccka_debug_trace_flat
             tf.argtypes = [C.c_void_p, C.c_int32]
@@ -358,7 +375,10 @@ def main():
             "data": "synthetic (on-device Philox load traces, seed 20251205)",
             "config": {"workload": (workloads[cfg].replace("HPA", "KEDA ScaledObject (scale to zero)") if args.keda
                                     else workloads[cfg].replace("1 deployment", f"{args.deployments} HPA deployments "
-                                                                f"sharing {spec.max_nodes} node slots")
+                                                                f"sharing {spec.max_nodes} node slots"
+                                                                + (" (demo_30 burst shape: alternating spot / "
+                                                                   "on-demand, 5 replicas, max 10)"
+                                                                   if args.deployments > 4 else ""))
                                     if args.deployments > 1 else workloads[cfg]) + (" + Karpenter drift at the zone switch" if args.drift else "")
                        + (" + replacement consolidation" if args.replace else "")
                        + (" + multi-node consolidation" if args.multi else "")
@@ -367,7 +387,10 @@ def main():
 ,
                        "scenarios_per_gpu": N, "steps_per_rollout": T,
                        "mode": "trajectory" if traj else "summary",
-                       "trace_layout": "[T][N] (shared traces)" if cfg == 4 else "[T][N]" if args.trace_flat else "wave-tiled [wave][T][lanes] (built by the first rollout)",
+                       "schedule": ("lane-skewed" if engine_id == 5 else "lockstep" if engine_id == 1 else "lane-skewed (single deployment)"
+                                    if engine_id == 2 else None),
+                       "trace_layout": "[T][N] (shared traces)" if cfg == 4 else "[T][N]" if args.trace_flat else
+                       "[T][D][N]" if engine_id in (1, 5) else "wave-tiled [wave][T][lanes] (built by the first rollout)",
                        "parallelism": f"scenario-sharded x{world}", "rccl_nranks": rccl.get("nranks")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -375,6 +398,8 @@ def main():
                          # not measured in this run: copied from the committed profile named here
                          "traffic_source": traffic_src,
                          "kernel": "rollout_d1_kernel<8,2>" if engine_id == 2 else
+                                   "rollout_kernel<%d,%d,0,1> (lane-skewed)" % general_dims(len(spec.deploys), spec.max_nodes)
+                                   if engine_id == 5 else
                                    "rollout_kernel<%d,%d>" % general_dims(len(spec.deploys), spec.max_nodes),
                          "kernel_ms_avg": avg_ms, "argmin_table_ms": table_ms,
                          "bytes_per_launch": bytes_launch},

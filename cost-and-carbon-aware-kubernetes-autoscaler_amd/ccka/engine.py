@@ -277,7 +277,8 @@ class Engine:
         return y
 
     def set_engine(self, mode: int):
-        """Internal: 0 = automatic engine choice, 1 = general kernel only."""
+        """Internal: 0 = automatic engine choice, 1 = general kernel only, 2 = the
+        general kernel in lockstep (no lane-skewed schedule for several deployments)."""
         self.lib.ccka_debug_engine.argtypes = [C.c_void_p, C.c_int32]
         self._chk(self.lib.ccka_debug_engine(self.ctx, mode), "ccka_debug_engine")
 
@@ -299,7 +300,9 @@ class Engine:
 
     def last_engine(self):
         """Internal: (engine, table_ms) of the last rollout; engine 1 = general
-        kernel, 2 = single-deployment kernel (rollout_d1.hip)."""
+        kernel, 2 = single-deployment kernel (rollout_d1.hip), 3 / 4 = the
+        launched / fused closed loop, 5 = the general kernel on the lane-skewed
+        schedule (rollout_sk.hip)."""
         e, ms = C.c_int32(), C.c_double()
         self._chk(self.lib.ccka_debug_last_engine(self.ctx, C.byref(e), C.byref(ms)),
                   "ccka_debug_last_engine")

@@ -60,6 +60,11 @@ struct ccka_ctx {
   int32_t* d_load_w = nullptr;
   int64_t load_w_count = 0;
   int32_t load_w_lpw = 0;  // lanes per wave it was tiled for (0: stale)
+  // scenario-major copy [NL][T][DP] of the trace for the general kernel's
+  // lane-skewed schedule (sk_trace); load_nt_dp = the DP it was built for (0: stale)
+  int32_t* d_load_nt = nullptr;
+  int64_t load_nt_count = 0;
+  int32_t load_nt_dp = 0;
   bool trace_flat = false;  // ccka_debug_trace_flat: read [T][N] (A/B of the layout)
   void* d_res = nullptr;  // one allocation, SoA carve
   KParams kp{};
@@ -103,7 +108,7 @@ struct ccka_ctx {
   int32_t* d_jtab2 = nullptr;
   double* d_wc0 = nullptr;    // one zero carbon weight (the offer table's score is the price)
   int JT = 0, NW = 0;
-  int engine_mode = 0;       // 0 auto, 1 general kernel only (ccka_debug_engine)
+  int engine_mode = 0;       // 0 auto, 1 general kernel only, 2 general kernel in lockstep (ccka_debug_engine)
   unsigned long long* d_stamps = nullptr;
   int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
   int occ = 0;               // its register-allocation occupancy target (0 = automatic)
@@ -621,6 +626,7 @@ void ccka_close(ccka_ctx* c) {
   dfree(c->d_world); dfree(c->d_types); dfree(c->d_price); dfree(c->d_ci_gpwh); dfree(c->d_ci_gpwmin);
   dfree(c->d_region); dfree(c->d_target); dfree(c->d_maxr); dfree(c->d_dstab); dfree(c->d_resetca);
   dfree(c->d_pswitch); dfree(c->d_cw); dfree(c->d_capsel); dfree(c->d_load); dfree(c->d_load_w); dfree(c->d_totals);
+  dfree(c->d_load_nt);
   dfree(c->d_ptable); dfree(c->d_pjtab); dfree(c->d_pwc);
   dfree(c->d_sinq);
   dfree(c->d_acc); dfree(c->d_order); dfree(c->d_cap1s); dfree(c->d_cap1t); dfree(c->d_zmasks); dfree(c->d_wc1000);
@@ -819,6 +825,7 @@ int ccka_set_scenarios(ccka_ctx* c, const ccka_scenarios* sc) {
   dfree(c->d_load_w);
   c->load_w_count = 0;
   c->load_w_lpw = 0;
+  c->load_nt_dp = 0;
   c->have_load = false;
   c->have_sc = true;
   c->ran = false;
@@ -897,6 +904,29 @@ static int d1_trace_tile(ccka_ctx* c) {
   return CCKA_OK;
 }
 
+// the skewed schedule's scenario-major trace copy (built once per trace: N*T*DP*4
+// bytes; without memory for it the kernel gathers from [T][D][N], same results)
+static int sk_trace(ccka_ctx* c) {
+  int dmax, nmax;
+  kernel_dims(c->hw.n_deploy, c->hw.max_nodes, &dmax, &nmax);
+  if (c->load_nt_dp == dmax && c->d_load_nt) return CCKA_OK;
+  const int64_t NL = load_cols(c), cnt = NL * c->hw.n_steps * dmax;
+  if (!c->d_load_nt || c->load_nt_count != cnt) {
+    dfree(c->d_load_nt);
+    c->load_nt_count = 0;
+    if (hipMalloc((void**)&c->d_load_nt, (size_t)cnt * 4) != hipSuccess) {
+      (void)hipGetLastError();
+      c->d_load_nt = nullptr;
+      return CCKA_OK;
+    }
+    c->load_nt_count = cnt;
+  }
+  HIPCHK(c, launch_trace_nt(c->d_load, c->d_load_nt, NL, c->hw.n_steps, c->hw.n_deploy, dmax, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->load_nt_dp = dmax;
+  return CCKA_OK;
+}
+
 int ccka_set_load(ccka_ctx* c, const int32_t* load, int64_t count) {
   if (!c || !load) return CCKA_EINVAL;
   if (!c->have_sc) return fail(c, CCKA_ESTATE, "set_scenarios first");
@@ -905,6 +935,7 @@ int ccka_set_load(ccka_ctx* c, const int32_t* load, int64_t count) {
   if ((rc = ensure_load(c)) != CCKA_OK) return rc;
   if (count != c->load_count) return fail(c, CCKA_EINVAL, "load count %lld != T*D*N %lld", (long long)count, (long long)c->load_count);
   c->load_w_lpw = 0;
+  c->load_nt_dp = 0;
   HIPCHK(c, hipMemcpyAsync(c->d_load, load, (size_t)count * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_load = true;
@@ -933,6 +964,7 @@ int ccka_gen_load(ccka_ctx* c, const ccka_trace_gen* g) {
   gp.noise = g->noise_pm; gp.burst_prob = g->burst_prob_pm;
   gp.burst_mult = g->burst_mult_pm; gp.burst_len = g->burst_len;
   c->load_w_lpw = 0;
+  c->load_nt_dp = 0;
   HIPCHK(c, launch_gen_load(gp, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_load = true;
@@ -1088,6 +1120,25 @@ static int setup_general(ccka_ctx* c, int32_t trajectory, int* block_out, size_t
   return CCKA_OK;
 }
 
+// The general kernel's lane-skewed schedule (rollout_sk.hip) holds for worlds
+// of two or more deployments that are HPA-scaled or static, with one HPA
+// decision per step over the register history rings, every hour's price tiles
+// in LDS, no detail breakdown and no drift / replacement / multi-node
+// consolidation (rollout.hip, rollout_kernel's SK notes).
+static bool sk_eligible(const ccka_ctx* c) {
+  const ccka_world& w = c->hw;
+  const KParams& k = c->kp;
+  if (w.n_deploy < 2 || c->engine_mode == 2 || c->detail_on) return false;
+  if (k.nsub != 1 || k.hlen != 0 || !k.all_hours || (k.ablate & ~16) != 0) return false;  // 16: diagnostic counters
+  if (w.disrupt_ext & (CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE | CCKA_DISRUPT_MULTI)) return false;
+  for (int d = 0; d < w.n_deploy; ++d) {
+    const int sc = w.deploy[d].scaler;
+    if (sc != CCKA_SCALER_HPA && sc != CCKA_SCALER_STATIC) return false;
+    if (sc == CCKA_SCALER_HPA && w.deploy[d].target_util_pct <= 0) return false;
+  }
+  return true;
+}
+
 int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
   if (!c) return CCKA_EINVAL;
   if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
@@ -1172,12 +1223,19 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
       HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, 12 * sizeof(unsigned long long), c->stream));
       k.stamps = c->d_stamps;
     }
+    const bool sk = sk_eligible(c);
+    k.load_nt = nullptr;
+    if (sk) {
+      if ((rc = sk_trace(c)) != CCKA_OK) return rc;
+      if (c->load_nt_dp) k.load_nt = c->d_load_nt;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
-    HIPCHK(c, launch_rollout(k, block, lds, c->stream));
+    if (sk) HIPCHK(c, launch_rollout_sk(k, block, lds, c->stream));
+    else HIPCHK(c, launch_rollout(k, block, lds, c->stream));
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-    c->last_engine = 1;
-    c->traj_nt = false;
+    c->last_engine = sk ? 5 : 1;
+    c->traj_nt = sk;  // the skewed schedule writes scenario-major records
   }
   c->traj_valid = trajectory != 0;
   c->detail_valid = c->detail_on;
@@ -1287,11 +1345,15 @@ static int policy_loop(ccka_ctx* c, int32_t trajectory, int32_t record, const cc
   if (!c) return CCKA_EINVAL;
   c->pg_valid = false;  // the recorded features / actions are about to be overwritten
   if (!c->have_world || !c->have_sc) return fail(c, CCKA_ESTATE, "world/scenarios not set");
-  // the single-deployment kernel's tiled trace copy (N*T*4 bytes) is not read
-  // here: released for the loop's own arrays, rebuilt by the next rollout
+  // the single-deployment kernel's tiled trace copy (N*T*4 bytes) and the
+  // skewed schedule's scenario-major one are not read here: released for the
+  // loop's own arrays, rebuilt by the next rollout
   dfree(c->d_load_w);
   c->load_w_count = 0;
   c->load_w_lpw = 0;
+  dfree(c->d_load_nt);
+  c->load_nt_count = 0;
+  c->load_nt_dp = 0;
   if (!c->have_load) return fail(c, CCKA_ESTATE, "no load traces (ccka_set_load / ccka_gen_load)");
   if (!c->mlp_have_w) return fail(c, CCKA_ESTATE, "MLP weights not set (ccka_mlp_set_weights)");
   (void)hipSetDevice(c->device);
@@ -2372,14 +2434,17 @@ int ccka_debug_ablate(ccka_ctx* c, int32_t mask) {
 }
 
 // Internal (not in include/ccka.h): 0 = choose the engine automatically,
-// 1 = always the general kernel (tests compare both engines).
+// 1 = always the general kernel (tests compare both engines), 2 = the general
+// kernel in lockstep (no lane-skewed schedule for several deployments).
 int ccka_debug_engine(ccka_ctx* c, int32_t mode) {
-  if (!c || mode < 0 || mode > 1) return CCKA_EINVAL;
+  if (!c || mode < 0 || mode > 2) return CCKA_EINVAL;
   c->engine_mode = mode;
   return CCKA_OK;
 }
 
-// Internal: which engine ran last (1 general, 2 single-deployment) and the
+// Internal: which engine ran last (1 general, 2 single-deployment, 3 the
+// launched closed loop, 4 the fused closed loop, 5 the general kernel on the
+// lane-skewed schedule) and the
 // duration of its argmin-table kernel.
 int ccka_debug_last_engine(ccka_ctx* c, int32_t* engine, double* table_ms) {
   if (!c) return CCKA_EINVAL;

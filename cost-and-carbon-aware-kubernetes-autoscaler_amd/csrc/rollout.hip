@@ -86,6 +86,7 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+#ifndef CCKA_ROLLOUT_PART  // the other rollout_*.hip units include this file for the kernel template only
 __global__ void __launch_bounds__(256) gen_load_kernel(GenParams g) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int d = blockIdx.y;
@@ -114,6 +115,7 @@ __global__ void __launch_bounds__(256) gen_load_kernel(GenParams g) {
     g.out[((int64_t)t * g.D + d) * g.n + i] = (int32_t)val;
   }
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Rollout kernel
@@ -239,6 +241,24 @@ __device__ __forceinline__ int util_div(long long usage, long long den) {
   const long long num = usage * 100;
   if (num < 0x7fffffffLL && den < 0x7fffffffLL) return (int)((unsigned)num / (unsigned)den);
   return (int)(num / den);
+}
+
+// HPA proposal of one decision with a metric (replica_calculator.go
+// GetResourceReplicas, SEMANTICS 3.C): usage (already clamped by the pod CPU
+// limit) over `ready` pods, `cur` replicas; u = the utilisation. Phase C and
+// the skewed schedule's record rebuild share it (the same binary64 operations).
+__device__ __forceinline__ int hpa_prop(long long usage, int cur, int ready, int req, int target, double lo,
+                                        double hi, int& u) {
+  u = util_div(usage, (long long)ready * req);
+  const double ratio = (double)u / (double)target;
+  if (cur - ready > 0 && ratio > 1.0) {
+    const int nu = util_div(usage, (long long)cur * req);
+    const double nr = (double)nu / (double)target;
+    if ((lo <= nr && nr <= hi) || nr < 1.0) return cur;
+    return max(cur, (int)ceil(nr * (double)cur));
+  }
+  if (lo <= ratio && ratio <= hi) return cur;
+  return (int)ceil(ratio * (double)ready);
 }
 
 // HPA behavior rules of one direction, hoisted into registers. wmask bit k:
@@ -587,9 +607,22 @@ constexpr bool kGKS = false;
 // features, the MLP (MFMA, both 32-lane halves of the wave as two tiles) and
 // the action (1: policy_act_kernel's mapping, 2: policy_sample_kernel's
 // sampling) -- one launch instead of 4T + 1, the state never leaves registers.
-template <int DMAX, int MAXN, int POL = 0>
+// SK: lane-skewed schedule (several deployments, round 6): each lane keeps its
+// own step counter; a step whose outcome is fixed by the state of the lane's
+// last full step and the step's load samples (every HPA keeps its replica
+// count, no readiness / hour / peak-window / consolidation boundary, nothing
+// pending) is a *quiet step* (threshold compares, accounting, the record);
+// every other step stalls the lane, and the wave runs the full step for all
+// its stalled lanes together (the single-deployment kernel's event batching,
+// rollout_d1.hip, for D <= 16 deployments). Host-checked preconditions
+// (sk_eligible in ccka_abi.cpp): HPA / static deployments, one decision per
+// step over the register rings, every hour's price tiles in LDS, no detail,
+// drift, replacement or multi-node consolidation, the whole horizon in one
+// launch. Trajectory records scenario-major [N][T].
+template <int DMAX, int MAXN, int POL = 0, int SK = 0>
 __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout_kernel(KParams p) {
   static_assert(POL == 0 || (DMAX == 1 && MAXN <= 8), "fused closed loop: one deployment, <= 8 slots");
+  static_assert(SK == 0 || POL == 0, "the skewed schedule is the rule-based rollout's");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // world through the constant address space for rare (profile-switch) reads;
   // hot fields are hoisted into registers below
@@ -599,7 +632,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wid = tid >> 6;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
   const bool active = i < p.N;
-  DetailDev* const det = active && p.detail ? p.detail + i : nullptr;
+  DetailDev* const det = !SK && active && p.detail ? p.detail + i : nullptr;  // (SK worlds: no detail)
 
   Lds L;
   L.K = K;
@@ -636,6 +669,10 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   __syncthreads();
   L.rmin = s_rng[0] == 0x7fffffff ? 0 : s_rng[0];
   const int rl = active ? my_r - L.rmin : 0;
+  // price-tile row of this lane's region and hour: every hour staged
+  // (all_hours): tile_base + (rl * 24 + hour) * tile_ints, so lanes at
+  // different hours (SK) read their own; else the staged hour's tile of rl
+  int rlx = rl;
   const int tile_ints = K * Z * 2;
   int* const tile_base = L.tile;
   for (int x = tid; x < p.span * 24; x += blockDim.x) {
@@ -644,7 +681,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     s_ci[x * 2 + 1] = p.ci_gpwh[rg * 24 + x % 24];
   }
   __syncthreads();
-  L.rstride = p.all_hours ? 24 * tile_ints : tile_ints;
+  L.rstride = tile_ints;
   if (p.all_hours) {
     // small catalogs: stage every hour's tiles once -> no barrier in the step loop
     for (int rr = 0; rr < p.span; ++rr) {
@@ -681,9 +718,10 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     plimit[q] = gw->pools[q].limit_cpu_m;
   }
   const int pdb_pct = gw->pdb_min_available_pct;
-  const bool gdrift = (gw->disrupt_ext & CCKA_DISRUPT_DRIFT) != 0;
-  const bool greplace = (gw->disrupt_ext & CCKA_DISRUPT_REPLACE) != 0;
-  const bool gmulti = (gw->disrupt_ext & CCKA_DISRUPT_MULTI) != 0;
+  // (SK worlds have none of the three: their code folds away)
+  const bool gdrift = !SK && (gw->disrupt_ext & CCKA_DISRUPT_DRIFT) != 0;
+  const bool greplace = !SK && (gw->disrupt_ext & CCKA_DISRUPT_REPLACE) != 0;
+  const bool gmulti = !SK && (gw->disrupt_ext & CCKA_DISRUPT_MULTI) != 0;
   const int slo_util = gw->slo_util_pct;
   const int base_nodes = gw->base_nodes, base_type = gw->base_type;
 
@@ -876,7 +914,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     // the hour's price tiles (block-uniform: every lane is at the same minute)
     const int h0 = ((gw->start_minute + t0) % 1440) / 60;
     if (p.all_hours) {
-      L.tile = tile_base + h0 * tile_ints;
+      rlx = rl * 24 + max(hour, 0);  // the restored hour's row
     } else {
       for (int rr = 0; rr < p.span; ++rr) {
         const int rg = L.rmin + rr;
@@ -939,8 +977,294 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     for (int q = 0; q < 8; ++q) dst[q] = make_uint4(fw[4 * q], fw[4 * q + 1], fw[4 * q + 2], fw[4 * q + 3]);
   };
 
+  // ---- SK: the lane-skewed schedule's state ----
+  constexpr int SKS = SK ? (DMAX <= 2 ? 8 : DMAX <= 4 ? 4 : 2) : 1;  // quiet steps per iteration and lane
+  constexpr int SKD = SK ? DMAX : 1;
+  constexpr int UQ = 0x7fffffff;  // "any usage" threshold
+  int tl = t0;       // the lane's next step
+  bool ev = true;    // ... runs the full step
+  int nxt = 0;       // first step that needs the full step again
+  int tq = t0;       // quiet steps [tq, tl) not yet flushed into the per-step sums
+  // per deployment, from the lane's last full step: the step keeps the replica
+  // count iff usage < q_ulim and (usage >= q_pge or t <= q_hold); usage >=
+  // q_slo is an SLO miss; q_rcap = ready pods * CPU limit
+  int q_ulim[SKD], q_pge[SKD], q_hold[SKD], q_slo[SKD], q_rcap[SKD];
+  float q_R[SKD];          // max over ready slots of pods / allocatable CPU (saturation bound)
+  long long q_W[SKD];      // sum over ready slots of dyn_nw_per_m * pods
+  uint32_t q_usum[SKD];    // sum of the quiet steps' upp since the flush
+  uint32_t q_ran = 0;      // bit d: the deployment's HPA runs with a metric
+  long long q_sidle = 0, q_corr = 0;  // base + idle energy per step; saturated-step corrections
+  int q_pend = 0, q_reps = 0, q_w0 = 0;
+  bool q_sloall = false;   // pods pending: every step misses the SLO
+  int Lq[SKS][SKD];        // the next quiet steps' load samples
+  // diagnostic schedule counters (SK_STATS variant builds only, tools/sk_stats.py):
+  // stalls by the reason of the lane's last full step's nxt (0 disruption
+  // pending, 1 pods not placed, 2 consolidation wake, 3 node ready, 4 hour /
+  // peak boundary), 5 HPA outside its thresholds, 6 live lane-passes, 7 lane
+  // full steps, 8 lane quiet steps, 9 wave full-step runs, 10 wave passes
+#ifdef SK_STATS
+  constexpr bool kSKS = SK != 0;
+#else
+  constexpr bool kSKS = false;
+#endif
+  uint32_t sks_c[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int sks_why = 0;
+#pragma unroll
+  for (int d = 0; d < SKD; ++d) {
+    q_ulim[d] = 0; q_pge[d] = 0; q_hold[d] = 0; q_slo[d] = UQ; q_rcap[d] = UQ;
+    q_R[d] = 0.f; q_W[d] = 0; q_usum[d] = 0;
+#pragma unroll
+    for (int s = 0; s < SKS; ++s) Lq[s][d] = 0;
+  }
+  // per-step sums of the quiet steps [tq, tl) (SEMANTICS 3.H: integer sums, any order)
+  auto sk_flush = [&]() {
+    const int nq = tl - tq;
+    if (nq > 0) {
+      long long e = (long long)nq * q_sidle + q_corr;
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) e += (long long)q_usum[d] * q_W[d];
+      cost += (long long)nq * (burn + base_price);
+      energy_nw += e;
+      e_hour += e;
+      pend_min += (long long)nq * q_pend;
+      nmin_spot += nq * nsp;
+      nmin_od += nq * nod;
+      // the quiet steps pushed raw usages into the history rings: their
+      // proposals under the replica / ready counts they ran with (unchanged
+      // since the last full step)
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) {
+        if (d >= D || dep[d].scaler != CCKA_SCALER_HPA) continue;
+#pragma unroll
+        for (int k = 0; k < CCKA_HIST; ++k) {
+          if (k < nq && (recv[d] >> k & 1u)) {
+            int u;
+            rec[d][k] = hpa_prop(rec[d][k], replicas[d], rpods[d], dep[d].req_cpu, target[d], dep[d].lo, dep[d].hi, u);
+          }
+        }
+      }
+    }
+    q_corr = 0;
+#pragma unroll
+    for (int d = 0; d < SKD; ++d) q_usum[d] = 0;
+    tq = tl;
+  };
+  // exact dynamic energy of one step (SEMANTICS 3.H) for the given upp
+  auto sk_dyn = [&](const uint32_t (&upp)[SKD]) -> long long {
+    long long e = 0;
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n) {
+      if (!((used & rdy) >> n & 1u)) continue;
+      const ccka_itype& ty = L.types[ni_type(ninfo[n])];
+      long long use = 0;
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) if (d < D) use += (long long)npods[n][d] * upp[d];
+      e += ty.dyn_nw_per_m * min(use, (long long)ty.alloc_cpu_m);
+    }
+    return e;
+  };
+  // the quiet steps' caches after a full step at t (state final for the step)
+  auto sk_caches = [&](int t, bool peak) {
+    int pend = 0, reps = 0;
+    const bool unplaced = g_dirty;
+    q_ran = 0;
+    q_sidle = base_nw;
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n)
+      if (used >> n & 1u) q_sidle += L.types[ni_type(ninfo[n])].idle_nw;
+#pragma unroll
+    for (int d = 0; d < SKD; ++d) {
+      if (d >= D) continue;
+      const Dep& dp = dep[d];
+      const int cur = replicas[d], rd = rpods[d];
+      pend += cur - rd;
+      reps += cur;
+      long long W = 0;
+      float R = 0.f;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        if (!((used & rdy) >> n & 1u)) continue;
+        const ccka_itype& ty = L.types[ni_type(ninfo[n])];
+        W += ty.dyn_nw_per_m * (long long)npods[n][d];
+        R = fmaxf(R, ty.alloc_cpu_m > 0 ? (float)npods[n][d] / (float)ty.alloc_cpu_m : 1e30f);
+      }
+      q_W[d] = W;
+      q_R[d] = R;
+      q_rcap[d] = dp.limit > 0 ? (int)min((long long)rd * dp.limit, (long long)UQ) : UQ;
+      int ulim = UQ, pge = 0, slo_thr = UQ, hold = UQ;
+      if (dp.scaler == CCKA_SCALER_HPA) {
+        const int minr = dp.minr, mx = maxr[d], tg = target[d];
+        const bool hpa_path = !(cur == 0 && minr != 0);
+        if (hpa_path && (cur > mx || cur < minr)) {
+          ulim = 0;  // the clamp moves the count: never quiet
+        } else if (hpa_path && rd > 0) {
+          q_ran |= 1u << d;
+          // the tolerance band as utilisations: lo <= fl(u / tg) <= hi <=> ulo <= u <= uhi
+          int ulo = max(0, (int)floor(dp.lo * (double)tg) - 2);
+          while ((double)ulo / (double)tg < dp.lo) ++ulo;
+          int uhi = (int)floor(dp.hi * (double)tg) + 2;
+          while ((double)uhi / (double)tg > dp.hi) --uhi;
+          // smallest usage with floor(100 usage / den) >= u (u >= 0)
+          auto umin = [](long long u, long long den) -> int {
+            return u <= 0 ? 0 : (int)min((u * den + 99) / 100, (long long)UQ);
+          };
+          const long long dreq = (long long)rd * dp.req_cpu;
+          int lim;
+          if (cur > rd) {
+            // unready pods: util <= target proposes ceil(util * ready / target) < cur
+            // below the band; util > target counts every replica (nu): keep iff nu <= uhi
+            pge = umin(ulo, dreq);
+            lim = max(umin((long long)tg + 1, dreq), umin((long long)uhi + 1, (long long)cur * dp.req_cpu));
+            slo_thr = 0;
+          } else {
+            // below the band the proposal ceil(fl(fl(u / tg) * cur)) reaches cur from
+            // some u* <= ulo on (monotone in u; found with the spec's own arithmetic)
+            auto prop = [&](int u) { return (int)ceil(((double)u / (double)tg) * (double)cur); };
+            int us = (int)(((long long)(cur - 1) * tg) / cur) + 1;
+            us = min(us, ulo);
+            while (us > 0 && prop(us - 1) >= cur) --us;
+            while (us < ulo && prop(us) < cur) ++us;
+            pge = umin(us, dreq);
+            lim = umin((long long)uhi + 1, dreq);
+            slo_thr = umin((long long)slo_util + 1, dreq);
+          }
+          ulim = cur >= mx ? UQ : lim;
+          if (cur <= minr) {
+            hold = UQ;  // a lower proposal cannot go below minReplicas = cur
+          } else {
+            // newest down-window record >= cur: held while it stays inside the window
+            const int nw = __popc((uint32_t)dnmask[d]);
+            hold = -0x40000000;
+#pragma unroll
+            for (int k = CCKA_HIST - 1; k >= 0; --k)
+              if (k < nw && (recv[d] >> k & 1u) && rec[d][k] >= cur) hold = t - k + nw;
+          }
+        }
+      }
+      q_ulim[d] = ulim;
+      q_pge[d] = pge;
+      q_slo[d] = slo_thr;
+      q_hold[d] = hold;
+    }
+    q_pend = pend;
+    q_reps = reps;
+    q_sloall = pend > 0;
+    q_w0 = 0xFFFF | (int)((peak ? 1u : 0u) << 16);
+    // first step that needs the full step again: a node becomes ready, the
+    // next clock hour or peak-window boundary, a ready node that the
+    // disruption gate admits becomes a consolidation candidate, or the next
+    // step while the disruption phase has work (g_dirty). Pods left pending
+    // by this step stay pending until one of these: the scheduler and
+    // Karpenter (phases E, F1, F2) placed or claimed all they could this step,
+    // and with the same nodes, prices and pools they do the same again.
+    const int mn = minute;
+    int nx = min(next_ready, t + 60 - mn % 60);
+    if (pswitch) {
+      const int dps = (ps - mn + 1439) % 1440 + 1, dpe = (pe - mn + 1439) % 1440 + 1;
+      nx = min(nx, t + min(dps, dpe));
+    }
+    {
+      // the gate of phase G (several deployments: a necessary condition for a
+      // deletion): a candidate that is empty, or of a WhenEmptyOrUnderutilized
+      // pool with its pods' CPU / memory / count within the free resources of
+      // the other ready slots of the capacity types its deployments admit. A
+      // candidate the gate rejects leaves the evaluation nothing to do (the
+      // evaluation at any step is exact, skipping it only when it would act
+      // on nothing), so only gate-admitted candidates wake the lane.
+      auto node_use = [&](int n, int& c, int& m, int& pods) {
+        c = 0; m = 0; pods = 0;
+#pragma unroll
+        for (int e = 0; e < SKD; ++e) {
+          const int k = e < D ? npods[n][e] : 0;
+          c += k * dep[e].req_cpu;
+          m += k * dep[e].req_mem;
+          pods += k;
+        }
+      };
+      int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        if (!((used & rdy) >> n & 1u)) continue;
+        int c, m, pods;
+        node_use(n, c, m, pods);
+        const ccka_itype& ty = L.types[ni_type(ninfo[n])];
+        const bool od = ni_cap(ninfo[n]) != 0;
+        const int fc = ty.alloc_cpu_m - c, fmm = ty.alloc_mem_mi - m, fp = ty.max_pods - pods;
+        ac0 += od ? 0 : fc; ac1 += od ? fc : 0;
+        am0 += od ? 0 : fmm; am1 += od ? fmm : 0;
+        ap0 += od ? 0 : fp; ap1 += od ? fp : 0;
+      }
+#pragma unroll
+      for (int n = 0; n < MAXN; ++n) {
+        if (!((used & rdy) >> n & 1u)) continue;
+        const uint32_t x = ninfo[n];
+        int ca = 0, pol = 0;
+#pragma unroll
+        for (int q = 0; q < CCKA_MAX_POOLS; ++q)
+          if (q == ni_pool(x)) { ca = pca[q]; pol = ppol[q]; }
+        const int thr = max(nready[n], nlast[n] + (ca + CCKA_STEP_SECONDS - 1) / CCKA_STEP_SECONDS);
+        if (thr <= t) continue;  // a candidate already: evaluated with this state
+        int c, m, pods;
+        node_use(n, c, m, pods);
+        bool pass = pods == 0;
+        if (!pass && pol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) {
+          uint32_t cs = 0;
+#pragma unroll
+          for (int e = 0; e < SKD; ++e) cs |= (e < D && npods[n][e] > 0) ? capsel[e] : 0u;
+          const bool s0 = (cs & capbit(0)) != 0, s1 = (cs & capbit(1)) != 0;
+          int vc = (s0 ? ac0 : 0) + (s1 ? ac1 : 0), vm = (s0 ? am0 : 0) + (s1 ? am1 : 0);
+          int vp = (s0 ? ap0 : 0) + (s1 ? ap1 : 0);
+          if (cs & capbit(ni_cap(x))) {
+            const ccka_itype& ty = L.types[ni_type(x)];
+            vc -= ty.alloc_cpu_m - c;
+            vm -= ty.alloc_mem_mi - m;
+            vp -= ty.max_pods - pods;
+          }
+          pass = c <= vc && m <= vm && pods <= vp;
+        }
+        if (pass) nx = min(nx, thr);
+      }
+    }
+    if (unplaced) nx = t + 1;
+    if constexpr (kSKS) {
+      bool unpl = false;
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) unpl = unpl || (d < D && placed[d] != replicas[d]);
+      // 1: pending pods (no longer a stall reason: counts full steps due to the rest while pods wait)
+      sks_why = g_dirty ? 0 : nx == next_ready ? 3 : nx == t + 60 - mn % 60 ? 4 : unpl ? 1 : 2;
+    }
+    nxt = nx;
+  };
+
   unsigned long long gst[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, glast = kGKS ? __builtin_amdgcn_s_memtime() : 0ull;
-  for (int t = t0; t < t1; ++t, minute = minute == 1439 ? 0 : minute + 1) {
+  for (int tt = t0;;) {
+    int t = tt;
+    bool stepl = active;  // this lane runs the full step of t in this pass
+    if constexpr (SK) {
+      const bool live = active && tl < t1;
+      if (__ballot(live) == 0) break;
+      t = tl;
+      stepl = live && ev;
+      GK_STAMP(7);  // SK: the quiet samples issued, loop top
+      if constexpr (kSKS) {
+        sks_c[6] += live ? 1 : 0;
+        sks_c[7] += stepl ? 1 : 0;
+        const unsigned long long bs = __ballot(stepl), bl = __ballot(live);
+        const bool lead = lane == __ffsll((long long)bl) - 1;
+        sks_c[9] += (lead && bs) ? 1 : 0;
+        sks_c[10] += lead ? 1 : 0;
+      }
+    } else {
+      if (tt >= t1) break;
+    }
+    if (!SK || __ballot(stepl) != 0) {
+    const bool active = stepl;  // the rest of the step is this lane's only when it runs it
+    if constexpr (SK) {
+      if (active) {
+        sk_flush();
+        minute = (gw->start_minute + t) % 1440;
+      }
+    }
     if constexpr (POL != 0) {
       // ---- the learned policy chooses step t's HPA target and carbon weight ----
       pbf16x8 w1b0[MLP_IN / 16];  // W1's first row block, in flight under the features
@@ -1037,17 +1361,22 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     int Lcur[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
-      Lcur[d] = Lnext[d];
-      // unconditional (clamped) load: lets the compiler count vmcnt exactly
-      // instead of draining every outstanding store at the loop back-edge
-      const int tn = t + 1 < p.T ? t + 1 : t;
-      Lnext[d] = lptr[((int64_t)tn * D + (d < D ? d : 0)) * lstride];
+      if constexpr (SK) {  // this lane's step
+        Lcur[d] = p.load_nt ? p.load_nt[(lcol * (int64_t)p.T + min(t, p.T - 1)) * DMAX + d]
+                            : lptr[((int64_t)min(t, p.T - 1) * D + (d < D ? d : 0)) * lstride];
+      } else {
+        Lcur[d] = Lnext[d];
+        // unconditional (clamped) load: lets the compiler count vmcnt exactly
+        // instead of draining every outstanding store at the loop back-edge
+        const int tn = t + 1 < p.T ? t + 1 : t;
+        Lnext[d] = lptr[((int64_t)tn * D + (d < D ? d : 0)) * lstride];
+      }
     }
     const int h = minute / 60;
     if (h != hour) {  // block-uniform: this hour's price tiles
       hour = h;
-      if (p.all_hours) {
-        L.tile = tile_base + h * tile_ints;
+      if (SK || p.all_hours) {
+        rlx = rl * 24 + h;
       } else {
         __syncthreads();
         for (int rr = 0; rr < p.span; ++rr) {
@@ -1072,13 +1401,13 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         }
         ci_gpwmin = s_ci[(rl * 24 + h) * 2 + 0];
         ci_gpwh = s_ci[(rl * 24 + h) * 2 + 1];
-        base_price = (long long)base_nodes * tprice(L, rl, base_type, 0, 1);
+        base_price = (long long)base_nodes * tprice(L, rlx, base_type, 0, 1);
         burn = 0;
         if (greplace) g_dirty = true;  // replacement offers depend on this hour's prices
 #pragma unroll
         for (int n = 0; n < MAXN; ++n) {
           if (used >> n & 1u) {
-            nprice[n] = tprice(L, rl, ni_type(ninfo[n]), ni_zone(ninfo[n]), ni_cap(ninfo[n]));
+            nprice[n] = tprice(L, rlx, ni_type(ninfo[n]), ni_zone(ninfo[n]), ni_cap(ninfo[n]));
             burn += nprice[n];
           }
         }
@@ -1130,7 +1459,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       }
       GK_STAMP(1);  // readiness, profile
       // ---- C. scalers: nsub decisions on the step's metric sample ----
-      for (int sub = 0; sub < p.nsub; ++sub) {
+      for (int sub = 0; sub < (SK ? 1 : p.nsub); ++sub) {  // SK: one decision per step
       if (sub > 0) {
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) { util_valid[d] = 0; util[d] = 0; kact_any[d] = false; }
@@ -1141,6 +1470,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         const Dep& dp = dep[d];
         const int Lv = Lcur[d];
         if (dp.scaler != CCKA_SCALER_HPA && dp.scaler != CCKA_SCALER_KEDA) continue;  // static / trigger
+        if (SK && dp.scaler != CCKA_SCALER_HPA) continue;  // (SK worlds have none)
         const int ready = rpods[d];
         const int cur = replicas[d];
         int desired = cur, proposal = cur;
@@ -1155,20 +1485,10 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           else if (ready > 0) {
             long long usage = Lv;
             if (dp.limit > 0) usage = min(usage, (long long)ready * dp.limit);
-            const int u = util_div(usage, (long long)ready * dp.req_cpu);
+            int u;
+            proposal = hpa_prop(usage, cur, ready, dp.req_cpu, target[d], dp.lo, dp.hi, u);
             util_valid[d] = 1;
             util[d] = u;
-            const double ratio = (double)u / (double)target[d];
-            if (cur - ready > 0 && ratio > 1.0) {
-              const int nu = util_div(usage, (long long)cur * dp.req_cpu);
-              const double nr = (double)nu / (double)target[d];
-              if ((dp.lo <= nr && nr <= dp.hi) || nr < 1.0) proposal = cur;
-              else proposal = max(cur, (int)ceil(nr * (double)cur));
-            } else if (dp.lo <= ratio && ratio <= dp.hi) {
-              proposal = cur;
-            } else {
-              proposal = (int)ceil(ratio * (double)ready);
-            }
             do_behavior = true;
           }
         } else {  // KEDA: own trigger + the KEDA_TRIGGER entries right after d
@@ -1211,7 +1531,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
             }
           }
         }
-        if (do_behavior && !ablated(p.ablate, 8) && p.hlen) {
+        if (do_behavior && !ablated(p.ablate, 8) && !SK && p.hlen) {
           ran = true;
           const ccka_deployment& gd = gw->deploy[d];
           const int dstab = p.down_stab && dp.scaler == CCKA_SCALER_HPA ? (int)p.down_stab[i] : gd.down.stab_window_s;
@@ -1235,7 +1555,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           else if (rc < cur) lo = max(lo, min(rate_limit(dp.dn, false, cur, delta[d]), cur));
           desired = rc < lo ? lo : (rc > hi ? hi : rc);
         }
-        if (p.hlen) {  // HBM history: this decision at hpos
+        if (!SK && p.hlen) {  // HBM history: this decision at hpos
           int2 e;
           e.x = ran ? proposal + 1 : 0;
           e.y = (hpa_path && desired != cur) ? desired - cur : 0;
@@ -1251,7 +1571,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         if (desired != cur) g_dirty = true;  // PDB expectation changed
         replicas[d] = desired;
       }
-      if (p.hlen) hpos = hpos + 1 == p.hlen ? 0 : hpos + 1;
+      if (!SK && p.hlen) hpos = hpos + 1 == p.hlen ? 0 : hpos + 1;
       }  // sub-steps
       GK_STAMP(2);  // scalers
       // ---- D. ReplicaSet reconcile (nominated first, then running; high slot first) ----
@@ -1401,7 +1721,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         const int ld = __ffsll((long long)need) - 1;
         need &= need - 1;
         // broadcast the leader's state
-        const int lrl = rdl(rl, ld);
+        const int lrl = rdl(rlx, ld);
         const double lwc = rdld(wc1000, ld);
         const double lci = rdld(ci_gpwh, ld);
         uint32_t lfree = rdlu(free_mask, ld);
@@ -1693,7 +2013,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #pragma unroll
               for (int c = 0; c < 2; ++c) {
                 if (!(cm & capbit(c))) continue;
-                const int pr = tprice(L, rl, k, z, c);
+                const int pr = tprice(L, rlx, k, z, c);
                 if (pr > 0 && (bk < 0 || pr < bpr)) { bk = k; bz = z; bc = c; bpr = pr; }
               }
             }
@@ -1711,7 +2031,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
               if (type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, 0, 0) < 0) continue;
               if (!limit_ok(L, k, use, limit, usem, limitm)) continue;
               for (int z = 0; z < L.Z; ++z)
-                if ((zm >> z & 1u) && tprice(L, rl, k, z, 0) > 0) { spot_only = true; break; }
+                if ((zm >> z & 1u) && tprice(L, rlx, k, z, 0) > 0) { spot_only = true; break; }
             }
           }
           double bs = 0.0;
@@ -1724,7 +2044,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #pragma unroll
               for (int c = 0; c < 2; ++c) {
                 if (!(cm & capbit(c)) || (spot_only && c != 0)) continue;
-                const int pr = tprice(L, rl, k, z, c);
+                const int pr = tprice(L, rlx, k, z, c);
                 if (pr <= 0) continue;
                 const double score = (double)pr + wc1000 * carbon;
                 if (bk < 0 || score < bs) { bk = k; bz = z; bc = c; bpr = pr; bs = score; }
@@ -2524,10 +2844,140 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         rcd.nodes_od = (uint16_t)nod;
         rcd.last_type = (uint16_t)step_last_type;
         rcd.flags = (uint16_t)flags;
-        *reinterpret_cast<int4*>(&p.traj[(int64_t)t * p.N + i]) = *reinterpret_cast<int4*>(&rcd);
+        // SK: scenario-major [N][T] (a lane's steps fill whole lines however far the lanes drift apart)
+        const int64_t ri = SK ? i * (int64_t)p.T + t : (int64_t)t * p.N + i;
+        *reinterpret_cast<int4*>(&p.traj[ri]) = *reinterpret_cast<int4*>(&rcd);
       }
     }
     GK_STAMP(6);  // accounting, record
+    if constexpr (SK) {
+      if (active) {
+        sk_caches(t, (flags & 1u) != 0);
+        tl = t + 1;
+        tq = tl;
+        ev = false;
+      }
+      GK_STAMP(9);  // SK: the quiet steps' caches
+    }
+    }  // the full step
+    if constexpr (SK) {
+      // this pass's quiet-step samples, steps tl .. tl + SKS - 1 (loaded after
+      // the full steps: held across them they would spill): from the
+      // scenario-major copy, one contiguous run per lane ([NL][T][DMAX]), or
+      // gathered from [T][D][N]
+      if (p.load_nt) {
+        const int32_t* b = p.load_nt + lcol * (int64_t)p.T * DMAX;
+#pragma unroll
+        for (int s = 0; s < SKS; ++s) {
+          const int ts = min(tl + s, p.T - 1);
+          if constexpr (DMAX == 2) {
+            const int2 v = *reinterpret_cast<const int2*>(b + (int64_t)ts * 2);
+            Lq[s][0] = v.x;
+            Lq[s][1] = v.y;
+          } else {
+#pragma unroll
+            for (int q = 0; q < DMAX / 4; ++q) {
+              const int4 v = *reinterpret_cast<const int4*>(b + (int64_t)ts * DMAX + 4 * q);
+              Lq[s][4 * q] = v.x;
+              Lq[s][4 * q + 1] = v.y;
+              Lq[s][4 * q + 2] = v.z;
+              Lq[s][4 * q + 3] = v.w;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < SKS; ++s) {
+          const int ts = min(tl + s, p.T - 1);
+#pragma unroll
+          for (int d = 0; d < SKD; ++d) Lq[s][d] = lptr[((int64_t)ts * D + (d < D ? d : 0)) * lstride];
+        }
+      }
+      // ---- quiet steps: up to SKS per iteration and lane ----
+      // (a rolled loop over a shifting sample window: the unrolled one is SKS
+      // copies of the sub-step, code that the full steps' evict from the
+      // instruction cache every pass)
+#ifdef SK_QUNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+      for (int s = 0; s < SKS; ++s) {
+        if (active && !ev && tl < t1) {
+          const int tc = tl;
+          bool ok = tc < nxt;
+          int us[SKD];
+          bool ge[SKD];
+#pragma unroll
+          for (int d = 0; d < SKD; ++d) {
+            us[d] = 0;
+            ge[d] = false;
+            if (d >= D) continue;
+            us[d] = min(Lq[0][d], q_rcap[d]);
+            if (dep[d].scaler != CCKA_SCALER_HPA) continue;
+            ge[d] = us[d] >= q_pge[d];
+            ok = ok && (uint32_t)us[d] < (uint32_t)q_ulim[d] && (ge[d] || tc <= q_hold[d]);
+          }
+          if (ok) {
+            bool slo_b = q_sloall;
+            uint32_t upp[SKD];
+            float sat = 0.f;
+#pragma unroll
+            for (int d = 0; d < SKD; ++d) {
+              upp[d] = 0u;
+              if (d >= D) continue;
+              const int rd = rpods[d];
+              upp[d] = rd > 0 ? (uint32_t)max(us[d], 0) / (uint32_t)rd : 0u;
+              q_usum[d] += upp[d];
+              sat += (float)upp[d] * q_R[d];
+              if (dep[d].scaler != CCKA_SCALER_HPA) continue;
+              const bool ran = (q_ran >> d & 1u) != 0;
+              if (ge[d]) q_hold[d] = max(q_hold[d], tc + __popc((uint32_t)dnmask[d]));
+              slo_b = slo_b || us[d] >= q_slo[d];
+              // the decision's records: the raw usage (its proposal is computed at
+              // the next full step, sk_flush), no replica change
+#pragma unroll
+              for (int k = CCKA_HIST - 1; k > 0; --k) { rec[d][k] = rec[d][k - 1]; delta[d][k] = delta[d][k - 1]; }
+              rec[d][0] = ran ? us[d] : 0;
+              delta[d][0] = 0;
+              recv[d] = ((recv[d] << 1) | (ran ? 1u : 0u)) & 0xFFu;
+            }
+            if (__builtin_expect(sat >= 0.9999f, 0)) {  // a node may saturate: the exact per-node sum
+              long long lin = 0;
+#pragma unroll
+              for (int d = 0; d < SKD; ++d) lin += (long long)upp[d] * q_W[d];
+              q_corr += sk_dyn(upp) - lin;
+            }
+            slo += slo_b ? 1 : 0;
+            if (p.traj) {
+              const int4 r = make_int4(q_reps, q_pend, (nsp & 0xFFFF) | nod << 16, q_w0 | (slo_b ? (8 << 16) : 0));
+              *reinterpret_cast<int4*>(&p.traj[i * (int64_t)p.T + tc]) = r;
+            }
+            tl = tc + 1;
+            if constexpr (kSKS) sks_c[8]++;
+#pragma unroll
+            for (int q = 0; q + 1 < SKS; ++q) {
+#pragma unroll
+              for (int d = 0; d < SKD; ++d) Lq[q][d] = Lq[q + 1][d];
+            }
+          } else {
+            ev = true;
+            if constexpr (kSKS) {
+              if (tc >= nxt) {
+#pragma unroll
+                for (int r = 0; r < 5; ++r) sks_c[r] += sks_why == r ? 1 : 0;
+              } else {
+                sks_c[5]++;
+              }
+            }
+          }
+        }
+      }
+      GK_STAMP(8);  // SK: quiet steps
+    } else {
+      ++tt;
+      minute = minute == 1439 ? 0 : minute + 1;
+    }
   }
   if constexpr (kGKS) {
     if (p.stamps && lane == (__ffsll((long long)__ballot(1)) - 1)) {
@@ -2536,7 +2986,14 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       atomicAdd(&p.stamps[11], 1ull);  // waves
     }
   }
+  if constexpr (kSKS) {
+    if (p.stamps) {
+#pragma unroll
+      for (int k = 0; k < 11; ++k) atomicAdd(&p.stamps[k], (unsigned long long)sks_c[k]);
+    }
+  }
   if (!active) return;
+  if constexpr (SK) sk_flush();  // the quiet steps since the last full step
   if (p.state) state_io(true);
   if (p.feat || p.feat_rec) {  // policy features of step t1 (SEMANTICS 5)
     uint32_t fw[32];
@@ -2581,6 +3038,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   p.hash[i] = hash;
 }
 
+#ifndef CCKA_ROLLOUT_PART
 // ---------------------------------------------------------------------------
 // Totals: fixed-order block partials, then one ordered final pass.
 // ---------------------------------------------------------------------------
@@ -2677,37 +3135,21 @@ hipError_t launch_rollout(const KParams& p, int block, size_t lds, hipStream_t s
   (void)grid; (void)lds; (void)s;
   return hipErrorInvalidValue;
 #else
-  // the smallest instantiation that holds the world (kernel_dims)
+  // the smallest instantiation that holds the world (kernel_dims); four or
+  // more deployments: rollout_multi.hip
   int dmax, nmax;
   kernel_dims(p.D, p.maxn, &dmax, &nmax);
+  if (dmax >= 4) return launch_rollout_multi(p, block, lds, s);
   if (dmax == 1 && nmax == 8)
     hipLaunchKernelGGL((rollout_kernel<1, 8>), dim3(grid), dim3(block), lds, s, p);
   else if (dmax == 1)
     hipLaunchKernelGGL((rollout_kernel<1, 16>), dim3(grid), dim3(block), lds, s, p);
   else if (dmax == 2 && nmax == 8)
     hipLaunchKernelGGL((rollout_kernel<2, 8>), dim3(grid), dim3(block), lds, s, p);
-  else if (dmax == 2)
-    hipLaunchKernelGGL((rollout_kernel<2, 16>), dim3(grid), dim3(block), lds, s, p);
-  else if (dmax == 4 && nmax == 8)
-    hipLaunchKernelGGL((rollout_kernel<4, 8>), dim3(grid), dim3(block), lds, s, p);
-  else if (dmax == 4)
-    hipLaunchKernelGGL((rollout_kernel<4, 16>), dim3(grid), dim3(block), lds, s, p);
-  else if (dmax == 8)
-    hipLaunchKernelGGL((rollout_kernel<8, 16>), dim3(grid), dim3(block), lds, s, p);
   else
-    hipLaunchKernelGGL((rollout_kernel<16, 16>), dim3(grid), dim3(block), lds, s, p);
+    hipLaunchKernelGGL((rollout_kernel<2, 16>), dim3(grid), dim3(block), lds, s, p);
   return hipGetLastError();
 #endif
-}
-
-// the fused closed loop: the whole horizon in one launch, one 256-thread block
-// (4 waves, one per SIMD) per 256 scenarios
-hipError_t launch_rollout_policy(const KParams& p, size_t lds, int pol, hipStream_t s) {
-  const unsigned grid = (unsigned)((p.N + 255) / 256);
-  if (p.D != 1 || p.maxn > 8 || (pol != 1 && pol != 2)) return hipErrorInvalidValue;
-  if (pol == 1) hipLaunchKernelGGL((rollout_kernel<1, 8, 1>), dim3(grid), dim3(256), lds, s, p);
-  else hipLaunchKernelGGL((rollout_kernel<1, 8, 2>), dim3(grid), dim3(256), lds, s, p);
-  return hipGetLastError();
 }
 
 hipError_t launch_totals(const TotParams& q, int nparts, hipStream_t s) {
@@ -2715,5 +3157,7 @@ hipError_t launch_totals(const TotParams& q, int nparts, hipStream_t s) {
   hipLaunchKernelGGL(totals_final, dim3(1), dim3(64), 0, s, q, nparts);
   return hipGetLastError();
 }
+
+#endif  // CCKA_ROLLOUT_PART
 
 }  // namespace ccka
