@@ -978,21 +978,35 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   };
 
   // ---- SK: the lane-skewed schedule's state ----
-  constexpr int SKS = SK ? (DMAX <= 2 ? 8 : DMAX <= 4 ? 4 : 2) : 1;  // quiet steps per iteration and lane
+#ifndef SK_S_V  // A/B of the quiet steps per pass (variant builds): 32 samples held per lane
+// (two deployments x 8 / 16 / 32 quiet steps per pass: 31.4 / 29.0 / 31.3 ms at 1e5 x 1440)
+#define SK_S_V (32 / DMAX > 2 ? 32 / DMAX : 2)
+#endif
+  constexpr int SKS = SK ? (SK_S_V) : 1;  // quiet steps per iteration and lane
   constexpr int SKD = SK ? DMAX : 1;
   constexpr int UQ = 0x7fffffff;  // "any usage" threshold
+#ifndef SK_K_V  // full-step cadence in passes (variant builds)
+#define SK_K_V 1
+#endif
+  int skpass = 0;    // passes (wave-uniform)
   int tl = t0;       // the lane's next step
   bool ev = true;    // ... runs the full step
   int nxt = 0;       // first step that needs the full step again
   int tq = t0;       // quiet steps [tq, tl) not yet flushed into the per-step sums
   // per deployment, from the lane's last full step: the step keeps the replica
   // count iff usage < q_ulim and (usage >= q_pge or t <= q_hold); usage >=
-  // q_slo is an SLO miss; q_rcap = ready pods * CPU limit
-  int q_ulim[SKD], q_pge[SKD], q_hold[SKD], q_slo[SKD], q_rcap[SKD];
+  // q_slo is an SLO miss
+  int q_ulim[SKD], q_pge[SKD], q_hold[SKD], q_slo[SKD];
   float q_R[SKD];          // max over ready slots of pods / allocatable CPU (saturation bound)
   long long q_W[SKD];      // sum over ready slots of dyn_nw_per_m * pods
   uint32_t q_usum[SKD];    // sum of the quiet steps' upp since the flush
   uint32_t q_ran = 0;      // bit d: the deployment's HPA runs with a metric
+  uint32_t q_atmax = 0;    // bit d: at maxReplicas (a quiet step's proposal may exceed cur)
+  uint32_t q_rawm[SKD];    // ring entries pushed by quiet steps as raw usages (proposal != cur)
+  // the tolerance band as utilisations, per deployment (constant: the
+  // scenario's target): lo <= fl(u / target) <= hi <=> ulo <= u <= uhi;
+  // packed ulo | uhi << 16
+  uint32_t q_band[SKD];
   long long q_sidle = 0, q_corr = 0;  // base + idle energy per step; saturated-step corrections
   int q_pend = 0, q_reps = 0, q_w0 = 0;
   bool q_sloall = false;   // pods pending: every step misses the SLO
@@ -1011,10 +1025,20 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   int sks_why = 0;
 #pragma unroll
   for (int d = 0; d < SKD; ++d) {
-    q_ulim[d] = 0; q_pge[d] = 0; q_hold[d] = 0; q_slo[d] = UQ; q_rcap[d] = UQ;
-    q_R[d] = 0.f; q_W[d] = 0; q_usum[d] = 0;
+    q_ulim[d] = 0; q_pge[d] = 0; q_hold[d] = 0; q_slo[d] = UQ;
+    q_R[d] = 0.f; q_W[d] = 0; q_usum[d] = 0; q_rawm[d] = 0; q_band[d] = 0;
 #pragma unroll
     for (int s = 0; s < SKS; ++s) Lq[s][d] = 0;
+    if constexpr (SK) {
+      if (d < D && dep[d].scaler == CCKA_SCALER_HPA && target[d] > 0) {
+        const int tg = target[d];
+        int ulo = max(0, (int)floor(dep[d].lo * (double)tg) - 2);
+        while ((double)ulo / (double)tg < dep[d].lo) ++ulo;
+        int uhi = (int)floor(dep[d].hi * (double)tg) + 2;
+        while ((double)uhi / (double)tg > dep[d].hi) --uhi;
+        q_band[d] = (uint32_t)ulo | (uint32_t)uhi << 16;
+      }
+    }
   }
   // per-step sums of the quiet steps [tq, tl) (SEMANTICS 3.H: integer sums, any order)
   auto sk_flush = [&]() {
@@ -1029,24 +1053,39 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       pend_min += (long long)nq * q_pend;
       nmin_spot += nq * nsp;
       nmin_od += nq * nod;
-      // the quiet steps pushed raw usages into the history rings: their
-      // proposals under the replica / ready counts they ran with (unchanged
-      // since the last full step)
+      // the history rings: a quiet step pushed its proposal (cur) into the
+      // decision records, or, where the proposal differs from cur, its raw
+      // usage (q_rawm): converted here under the replica / ready counts the
+      // quiet steps ran with (unchanged since the last full step); their zero
+      // replica changes enter the change ring here, min(nq, 8) at once
+      const int m = min(nq, CCKA_HIST);
 #pragma unroll
       for (int d = 0; d < SKD; ++d) {
         if (d >= D || dep[d].scaler != CCKA_SCALER_HPA) continue;
+        if (q_rawm[d]) {
 #pragma unroll
-        for (int k = 0; k < CCKA_HIST; ++k) {
-          if (k < nq && (recv[d] >> k & 1u)) {
-            int u;
-            rec[d][k] = hpa_prop(rec[d][k], replicas[d], rpods[d], dep[d].req_cpu, target[d], dep[d].lo, dep[d].hi, u);
+          for (int k = 0; k < CCKA_HIST; ++k) {
+            if (q_rawm[d] >> k & 1u) {
+              int u;
+              rec[d][k] = hpa_prop(rec[d][k], replicas[d], rpods[d], dep[d].req_cpu, target[d], dep[d].lo, dep[d].hi, u);
+            }
           }
+        }
+#pragma unroll
+        for (int b = 4; b >= 1; b >>= 1) {
+          const bool sh = (m & b) != 0;
+#pragma unroll
+          for (int k = CCKA_HIST - 1; k >= 0; --k) delta[d][k] = sh ? (k >= b ? delta[d][k - (k >= b ? b : 0)] : 0) : delta[d][k];
+        }
+        if (m & 8) {
+#pragma unroll
+          for (int k = 0; k < CCKA_HIST; ++k) delta[d][k] = 0;
         }
       }
     }
     q_corr = 0;
 #pragma unroll
-    for (int d = 0; d < SKD; ++d) q_usum[d] = 0;
+    for (int d = 0; d < SKD; ++d) { q_usum[d] = 0; q_rawm[d] = 0; }
     tq = tl;
   };
   // exact dynamic energy of one step (SEMANTICS 3.H) for the given upp
@@ -1068,10 +1107,30 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
     int pend = 0, reps = 0;
     const bool unplaced = g_dirty;
     q_ran = 0;
-    q_sidle = base_nw;
+    q_atmax = 0;
+    // the slots' type fields, read once and unconditionally (an unused slot
+    // reads type 0 and contributes nothing): the LDS reads issue together
+    long long sidle = base_nw;
+    long long Wd[SKD];
+    float Rd[SKD];
 #pragma unroll
-    for (int n = 0; n < MAXN; ++n)
-      if (used >> n & 1u) q_sidle += L.types[ni_type(ninfo[n])].idle_nw;
+    for (int d = 0; d < SKD; ++d) { Wd[d] = 0; Rd[d] = 0.f; }
+#pragma unroll
+    for (int n = 0; n < MAXN; ++n) {
+      const ccka_itype& ty = L.types[ni_type(ninfo[n])];
+      const long long idle = ty.idle_nw, dyn = ty.dyn_nw_per_m;
+      const int acpu = ty.alloc_cpu_m;
+      const bool u = (used >> n & 1u) != 0, r = ((used & rdy) >> n & 1u) != 0;
+      sidle += u ? idle : 0;
+      const float ra = acpu > 0 ? __builtin_amdgcn_rcpf((float)acpu) : 1e30f;  // (a bound: the check keeps a margin)
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) {
+        const int k = d < D ? npods[n][d] : 0;
+        Wd[d] += r ? dyn * (long long)k : 0;
+        Rd[d] = r ? fmaxf(Rd[d], (float)k * ra) : Rd[d];
+      }
+    }
+    q_sidle = sidle;
 #pragma unroll
     for (int d = 0; d < SKD; ++d) {
       if (d >= D) continue;
@@ -1079,18 +1138,8 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       const int cur = replicas[d], rd = rpods[d];
       pend += cur - rd;
       reps += cur;
-      long long W = 0;
-      float R = 0.f;
-#pragma unroll
-      for (int n = 0; n < MAXN; ++n) {
-        if (!((used & rdy) >> n & 1u)) continue;
-        const ccka_itype& ty = L.types[ni_type(ninfo[n])];
-        W += ty.dyn_nw_per_m * (long long)npods[n][d];
-        R = fmaxf(R, ty.alloc_cpu_m > 0 ? (float)npods[n][d] / (float)ty.alloc_cpu_m : 1e30f);
-      }
-      q_W[d] = W;
-      q_R[d] = R;
-      q_rcap[d] = dp.limit > 0 ? (int)min((long long)rd * dp.limit, (long long)UQ) : UQ;
+      q_W[d] = Wd[d];
+      q_R[d] = Rd[d];
       int ulim = UQ, pge = 0, slo_thr = UQ, hold = UQ;
       if (dp.scaler == CCKA_SCALER_HPA) {
         const int minr = dp.minr, mx = maxr[d], tg = target[d];
@@ -1099,11 +1148,8 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           ulim = 0;  // the clamp moves the count: never quiet
         } else if (hpa_path && rd > 0) {
           q_ran |= 1u << d;
-          // the tolerance band as utilisations: lo <= fl(u / tg) <= hi <=> ulo <= u <= uhi
-          int ulo = max(0, (int)floor(dp.lo * (double)tg) - 2);
-          while ((double)ulo / (double)tg < dp.lo) ++ulo;
-          int uhi = (int)floor(dp.hi * (double)tg) + 2;
-          while ((double)uhi / (double)tg > dp.hi) --uhi;
+          q_atmax |= (cur >= mx ? 1u : 0u) << d;
+          const int ulo = (int)(q_band[d] & 0xFFFFu), uhi = (int)(q_band[d] >> 16);
           // smallest usage with floor(100 usage / den) >= u (u >= 0)
           auto umin = [](long long u, long long den) -> int {
             return u <= 0 ? 0 : (int)min((u * den + 99) / 100, (long long)UQ);
@@ -1117,13 +1163,16 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
             lim = max(umin((long long)tg + 1, dreq), umin((long long)uhi + 1, (long long)cur * dp.req_cpu));
             slo_thr = 0;
           } else {
-            // below the band the proposal ceil(fl(fl(u / tg) * cur)) reaches cur from
-            // some u* <= ulo on (monotone in u; found with the spec's own arithmetic)
-            auto prop = [&](int u) { return (int)ceil(((double)u / (double)tg) * (double)cur); };
-            int us = (int)(((long long)(cur - 1) * tg) / cur) + 1;
+            // below the band the proposal ceil(fl(fl(u / tg) * cur)) reaches cur
+            // from the smallest u with u * cur > (cur - 1) * tg on (the binary64
+            // rounding can move that only at an exact multiple, checked with the
+            // spec's own arithmetic); monotone in u, capped at the band
+            const uint32_t x = (uint32_t)(cur - 1) * (uint32_t)tg;  // < 2^31: cur, tg < 2^15
+            int us = (int)(x / (uint32_t)cur) + 1;
+            if (__builtin_expect((uint32_t)(us - 1) * (uint32_t)cur == x, 0) &&
+                (int)ceil(((double)(us - 1) / (double)tg) * (double)cur) >= cur)
+              --us;
             us = min(us, ulo);
-            while (us > 0 && prop(us - 1) >= cur) --us;
-            while (us < ulo && prop(us) < cur) ++us;
             pge = umin(us, dreq);
             lim = umin((long long)uhi + 1, dreq);
             slo_thr = umin((long long)slo_util + 1, dreq);
@@ -1181,48 +1230,47 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           pods += k;
         }
       };
+      // per ready slot: its free CPU / memory / pod count (the type's allocatable
+      // minus its pods' requests), summed by capacity type; branch-free, every
+      // slot's type read unconditionally so that the LDS reads issue together
+      int fcs[MAXN], fms[MAXN], fps[MAXN];
       int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        if (!((used & rdy) >> n & 1u)) continue;
+        const ccka_itype& ty = L.types[ni_type(ninfo[n])];
         int c, m, pods;
         node_use(n, c, m, pods);
-        const ccka_itype& ty = L.types[ni_type(ninfo[n])];
-        const bool od = ni_cap(ninfo[n]) != 0;
-        const int fc = ty.alloc_cpu_m - c, fmm = ty.alloc_mem_mi - m, fp = ty.max_pods - pods;
-        ac0 += od ? 0 : fc; ac1 += od ? fc : 0;
-        am0 += od ? 0 : fmm; am1 += od ? fmm : 0;
-        ap0 += od ? 0 : fp; ap1 += od ? fp : 0;
+        const bool r = ((used & rdy) >> n & 1u) != 0, od = ni_cap(ninfo[n]) != 0;
+        fcs[n] = ty.alloc_cpu_m - c;
+        fms[n] = ty.alloc_mem_mi - m;
+        fps[n] = ty.max_pods - pods;
+        ac0 += (r && !od) ? fcs[n] : 0; ac1 += (r && od) ? fcs[n] : 0;
+        am0 += (r && !od) ? fms[n] : 0; am1 += (r && od) ? fms[n] : 0;
+        ap0 += (r && !od) ? fps[n] : 0; ap1 += (r && od) ? fps[n] : 0;
       }
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
-        if (!((used & rdy) >> n & 1u)) continue;
         const uint32_t x = ninfo[n];
         int ca = 0, pol = 0;
 #pragma unroll
         for (int q = 0; q < CCKA_MAX_POOLS; ++q)
           if (q == ni_pool(x)) { ca = pca[q]; pol = ppol[q]; }
+        // a slot that is not yet a candidate (one already is: evaluated with this state)
         const int thr = max(nready[n], nlast[n] + (ca + CCKA_STEP_SECONDS - 1) / CCKA_STEP_SECONDS);
-        if (thr <= t) continue;  // a candidate already: evaluated with this state
         int c, m, pods;
         node_use(n, c, m, pods);
-        bool pass = pods == 0;
-        if (!pass && pol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED) {
-          uint32_t cs = 0;
+        uint32_t cs = 0;
 #pragma unroll
-          for (int e = 0; e < SKD; ++e) cs |= (e < D && npods[n][e] > 0) ? capsel[e] : 0u;
-          const bool s0 = (cs & capbit(0)) != 0, s1 = (cs & capbit(1)) != 0;
-          int vc = (s0 ? ac0 : 0) + (s1 ? ac1 : 0), vm = (s0 ? am0 : 0) + (s1 ? am1 : 0);
-          int vp = (s0 ? ap0 : 0) + (s1 ? ap1 : 0);
-          if (cs & capbit(ni_cap(x))) {
-            const ccka_itype& ty = L.types[ni_type(x)];
-            vc -= ty.alloc_cpu_m - c;
-            vm -= ty.alloc_mem_mi - m;
-            vp -= ty.max_pods - pods;
-          }
-          pass = c <= vc && m <= vm && pods <= vp;
-        }
-        if (pass) nx = min(nx, thr);
+        for (int e = 0; e < SKD; ++e) cs |= (e < D && npods[n][e] > 0) ? capsel[e] : 0u;
+        const bool s0 = (cs & capbit(0)) != 0, s1 = (cs & capbit(1)) != 0;
+        int vc = (s0 ? ac0 : 0) + (s1 ? ac1 : 0), vm = (s0 ? am0 : 0) + (s1 ? am1 : 0);
+        int vp = (s0 ? ap0 : 0) + (s1 ? ap1 : 0);
+        const bool own = (cs & capbit(ni_cap(x))) != 0;  // not a receiver of its own pods
+        vc -= own ? fcs[n] : 0;
+        vm -= own ? fms[n] : 0;
+        vp -= own ? fps[n] : 0;
+        const bool pass = pods == 0 || (pol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED && c <= vc && m <= vm && pods <= vp);
+        if (((used & rdy) >> n & 1u) && thr > t && pass) nx = min(nx, thr);
       }
     }
     if (unplaced) nx = t + 1;
@@ -1245,6 +1293,12 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       if (__ballot(live) == 0) break;
       t = tl;
       stepl = live && ev;
+      // full steps every SK_K_V passes (more stalled lanes per run), or at once
+      // when no live lane can step quietly
+      if constexpr (SK_K_V > 1) {
+        const bool due = (++skpass % SK_K_V) == 0 || __ballot(live && !ev) == 0;
+        stepl = stepl && due;
+      }
       GK_STAMP(7);  // SK: the quiet samples issued, loop top
       if constexpr (kSKS) {
         sks_c[6] += live ? 1 : 0;
@@ -2781,7 +2835,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         if (rd > 0) {
           long long usage = Lcur[d];
           if (dep[d].limit > 0) usage = min(usage, (long long)rd * dep[d].limit);
-          upp[d] = max(usage, 0LL) / rd;
+          upp[d] = (long long)((uint32_t)max(usage, 0LL) / (uint32_t)rd);  // usage <= INT32_MAX
         }
       }
       long long e_step = base_nw;
@@ -2913,7 +2967,8 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
             us[d] = 0;
             ge[d] = false;
             if (d >= D) continue;
-            us[d] = min(Lq[0][d], q_rcap[d]);
+            // usage clamped by the pods' CPU limit (ready pods * limit, 64-bit)
+            us[d] = dep[d].limit > 0 ? (int)min((long long)Lq[0][d], (long long)rpods[d] * dep[d].limit) : Lq[0][d];
             if (dep[d].scaler != CCKA_SCALER_HPA) continue;
             ge[d] = us[d] >= q_pge[d];
             ok = ok && (uint32_t)us[d] < (uint32_t)q_ulim[d] && (ge[d] || tc <= q_hold[d]);
@@ -2926,20 +2981,28 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
             for (int d = 0; d < SKD; ++d) {
               upp[d] = 0u;
               if (d >= D) continue;
-              const int rd = rpods[d];
-              upp[d] = rd > 0 ? (uint32_t)max(us[d], 0) / (uint32_t)rd : 0u;
+              // upp = floor(usage / ready): a binary32 reciprocal estimate and one
+              // remainder correction, exact while upp < 2^20 (else the division)
+              const int rd = max(rpods[d], 1);
+              const uint32_t a = (uint32_t)max(us[d], 0);
+              uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)rd));
+              const int rm = (int)(a - q * (uint32_t)rd);
+              q = q + (rm >= rd ? 1u : 0u) - (rm < 0 ? 1u : 0u);
+              if (__builtin_expect(q >= (1u << 20), 0)) q = a / (uint32_t)rd;
+              upp[d] = rpods[d] > 0 ? q : 0u;
               q_usum[d] += upp[d];
               sat += (float)upp[d] * q_R[d];
               if (dep[d].scaler != CCKA_SCALER_HPA) continue;
               const bool ran = (q_ran >> d & 1u) != 0;
+              // the proposal is cur from q_pge on below maxReplicas; else the raw
+              // usage goes into the record, its proposal computed at the flush
+              const bool raw = !ge[d] || (q_atmax >> d & 1u) != 0;
               if (ge[d]) q_hold[d] = max(q_hold[d], tc + __popc((uint32_t)dnmask[d]));
               slo_b = slo_b || us[d] >= q_slo[d];
-              // the decision's records: the raw usage (its proposal is computed at
-              // the next full step, sk_flush), no replica change
 #pragma unroll
-              for (int k = CCKA_HIST - 1; k > 0; --k) { rec[d][k] = rec[d][k - 1]; delta[d][k] = delta[d][k - 1]; }
-              rec[d][0] = ran ? us[d] : 0;
-              delta[d][0] = 0;
+              for (int k = CCKA_HIST - 1; k > 0; --k) rec[d][k] = rec[d][k - 1];
+              rec[d][0] = ran ? (raw ? us[d] : replicas[d]) : 0;
+              q_rawm[d] = ((q_rawm[d] << 1) | ((ran && raw) ? 1u : 0u)) & 0xFFu;
               recv[d] = ((recv[d] << 1) | (ran ? 1u : 0u)) & 0xFFu;
             }
             if (__builtin_expect(sat >= 0.9999f, 0)) {  // a node may saturate: the exact per-node sum
