@@ -1129,6 +1129,12 @@ static bool sk_eligible(const ccka_ctx* c) {
   const ccka_world& w = c->hw;
   const KParams& k = c->kp;
   if (w.n_deploy < 2 || c->engine_mode == 2 || c->detail_on) return false;
+  // up to four deployments: beyond, the per-lane state of the skewed schedule
+  // spills (8 x 16 slots: 5.6 KB per lane) and the lockstep kernel is faster
+  // (8 deployments 475 vs 307 ms, 12: 1039 vs 695 ms at 1e5 x 1440)
+  int dmax, nmax;
+  kernel_dims(w.n_deploy, w.max_nodes, &dmax, &nmax);
+  if (dmax > 4) return false;
   if (k.nsub != 1 || k.hlen != 0 || !k.all_hours || (k.ablate & ~16) != 0) return false;  // 16: diagnostic counters
   if (w.disrupt_ext & (CCKA_DISRUPT_DRIFT | CCKA_DISRUPT_REPLACE | CCKA_DISRUPT_MULTI)) return false;
   for (int d = 0; d < w.n_deploy; ++d) {

@@ -152,9 +152,8 @@ hipError_t launch_totals(const TotParams& q, int nparts, hipStream_t s);
 hipError_t launch_rollout_policy(const KParams& p, size_t lds, int pol, hipStream_t s);
 // four or more deployments, lockstep (rollout_multi.hip)
 hipError_t launch_rollout_multi(const KParams& p, int block, size_t lds, hipStream_t s);
-// two or more deployments on the lane-skewed schedule (rollout_sk.hip)
+// two to four deployments on the lane-skewed schedule (rollout_sk.hip)
 hipError_t launch_rollout_sk(const KParams& p, int block, size_t lds, hipStream_t s);
-hipError_t launch_rollout_sk16(const KParams& p, int block, size_t lds, hipStream_t s);  // 8 / 16 deployments
 // [T][D][NL] -> [NL][T][DP] (DP >= D, a power of two <= 16; padded with 0) for the skewed schedule
 hipError_t launch_trace_nt(const int32_t* in, int32_t* out, int64_t NL, int64_t T, int32_t D, int32_t DP,
                            hipStream_t s);

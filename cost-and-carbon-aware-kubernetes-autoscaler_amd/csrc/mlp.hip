@@ -301,6 +301,9 @@ __global__ void __launch_bounds__(256, 1) mlp16_kernel(MlpParams p) {
   constexpr int NO = MLP_HID / 16;                      // output tiles of layers 1 and 2
   constexpr int KS1 = MLP_IN / 32, KS2 = MLP_HID / 32;  // k-steps
   constexpr int PF = 2;                                 // W2 fragments in flight
+  // the output layer's k-step for tile t runs inside the W2 chain at s = t + 1
+  // (s < KS2): more tiles per pass would drop layer-3 terms
+  static_assert(T16 < KS2, "MLP16_T must stay below MLP_HID / 32");
   __shared__ __attribute__((aligned(16))) float s_b[2 * MLP_HID + 16];  // b1 | b2 | b3 (zero-padded to 16)
   __shared__ bf16x8 s_w3[KS2 * WAVE];                                   // 8 KiB
   __shared__ bf16x8 s_w2[NO * KS2 * WAVE];                              // 128 KiB

@@ -540,6 +540,9 @@ __device__ __forceinline__ pf32x16 mlp_tile(const pbf16x8 (&xf)[MLP_IN / 16], co
   // W2 fragments from LDS MLP_W2PF MFMAs ahead (one wave per SIMD: nothing
   // else hides an LDS read issued just before its MFMA)
   constexpr int PF = MLP_W2PF;
+  // the read-ahead ring is indexed by kk % PF for fragment m * KS2 + kk: that
+  // is the fragment's own slot only while PF divides KS2
+  static_assert(KS2 % PF == 0, "MLP_W2PF must divide MLP_HID / 16");
   pbf16x8 wq[PF];
 #pragma unroll
   for (int j = 0; j < PF; ++j) wq[j] = s_w2[j * 64 + lane];
@@ -607,14 +610,14 @@ constexpr bool kGKS = false;
 // features, the MLP (MFMA, both 32-lane halves of the wave as two tiles) and
 // the action (1: policy_act_kernel's mapping, 2: policy_sample_kernel's
 // sampling) -- one launch instead of 4T + 1, the state never leaves registers.
-// SK: lane-skewed schedule (several deployments, round 6): each lane keeps its
+// SK: lane-skewed schedule (two to four deployments, round 6): each lane keeps its
 // own step counter; a step whose outcome is fixed by the state of the lane's
 // last full step and the step's load samples (every HPA keeps its replica
 // count, no readiness / hour / peak-window / consolidation boundary, nothing
 // pending) is a *quiet step* (threshold compares, accounting, the record);
 // every other step stalls the lane, and the wave runs the full step for all
 // its stalled lanes together (the single-deployment kernel's event batching,
-// rollout_d1.hip, for D <= 16 deployments). Host-checked preconditions
+// rollout_d1.hip, for D <= 4 deployments). Host-checked preconditions
 // (sk_eligible in ccka_abi.cpp): HPA / static deployments, one decision per
 // step over the register rings, every hour's price tiles in LDS, no detail,
 // drift, replacement or multi-node consolidation, the whole horizon in one

@@ -1,5 +1,5 @@
 // rollout_sk.hip — the general kernel on the lane-skewed schedule
-// (rollout_kernel<DMAX, MAXN, 0, 1>, rollout.hip): worlds of two or more HPA /
+// (rollout_kernel<DMAX, MAXN, 0, 1>, rollout.hip): worlds of two to four HPA /
 // static deployments run their quiet steps per lane and their full steps in
 // per-wave batches of stalled lanes (the single-deployment kernel's event
 // batching, rollout_d1.hip, for several deployments). sk_eligible
@@ -64,8 +64,6 @@ hipError_t launch_rollout_sk(const KParams& p, int block, size_t lds, hipStream_
     hipLaunchKernelGGL((rollout_kernel<4, 8, 0, 1>), dim3(grid), dim3(block), lds, s, p);
   else if (dmax == 4)
     hipLaunchKernelGGL((rollout_kernel<4, 16, 0, 1>), dim3(grid), dim3(block), lds, s, p);
-  else if (dmax >= 8)  // rollout_sk16.hip (compiled in parallel)
-    return launch_rollout_sk16(p, block, lds, s);
   else
     return hipErrorInvalidValue;
 #endif

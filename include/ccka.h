@@ -252,9 +252,10 @@ typedef struct ccka_detail {
 
 /* Trajectory record, one per (step, scenario). 16 bytes. ccka_get_trajectory
  * returns them step-major [T][N]; on the device they stay in the layout the
- * engine wrote (ccka_trajectory_layout): the single-deployment engine writes
- * scenario-major [N][T] (each scenario's horizon contiguous), the general
- * engine step-major [T][N]. */
+ * engine wrote (ccka_trajectory_layout): the single-deployment engine and the
+ * general engine's lane-skewed schedule (worlds of several HPA / static
+ * deployments) write scenario-major [N][T] (each scenario's horizon
+ * contiguous), the general engine in lockstep step-major [T][N]. */
 enum { CCKA_TRAJ_TN = 0, CCKA_TRAJ_NT = 1 };
 typedef struct ccka_traj_rec {
   int32_t replicas;
@@ -338,7 +339,12 @@ int ccka_set_scenarios(ccka_ctx* ctx, const ccka_scenarios* sc);
 /* Upload host load traces, layout [T][D][N] int32. For a single-deployment
  * world with per-scenario traces the device also keeps a wave-tiled copy
  * (another T*N*4 bytes; the single-deployment kernel's read layout, built
- * here once per trace; without the memory for it that kernel reads [T][N]). */
+ * by the first rollout after each new trace; without the memory for it that
+ * kernel reads [T][N]). Worlds that run on the general kernel's lane-skewed
+ * schedule keep a scenario-major copy [N][T][DP] instead (DP = 2/4/8/16 >=
+ * the deployments; built the same way). ccka_policy_rollout and
+ * ccka_policy_grad release both copies for their own arrays: the next rollout
+ * rebuilds its copy (one transpose kernel, ~0.4 ms for 1e5 x 1440 x 1). */
 int ccka_set_load(ccka_ctx* ctx, const int32_t* load, int64_t count);
 /* Generate load traces on the device (same values as the host generator;
  * the same wave-tiled copy as ccka_set_load). */
@@ -401,7 +407,12 @@ int ccka_mlp_set_weights(ccka_ctx* ctx, int32_t in_dim, int32_t hidden, int32_t 
 /* Cluster states [n][in_dim] bf16: uploaded, or synthesised on the device. */
 int ccka_mlp_set_states(ccka_ctx* ctx, const uint16_t* x, int64_t n);
 int ccka_mlp_gen_states(ccka_ctx* ctx, int64_t n, uint64_t seed);
-/* actions = policy(states) on the device (bf16 MFMA, fp32 accumulation). */
+/* actions = policy(states) on the device (bf16 MFMA, fp32 accumulation). The
+ * standalone forward runs the 16x16x32 MFMA kernel; the policy loops keep the
+ * 32x32x16 accumulation order. On the same states the two differ only in fp32
+ * summation order (|dy| ~ 1e-3), which after the policy's rint can move an
+ * action: for a loop's final states, ccka_debug_mlp_tile(ctx, 32) (internal)
+ * makes the forward reproduce the loop's outputs bit for bit. */
 int ccka_mlp_forward(ccka_ctx* ctx);
 int ccka_mlp_forward_async(ccka_ctx* ctx);
 /* Copy the actions [n][out_dim] fp32 back. */

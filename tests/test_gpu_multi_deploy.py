@@ -46,7 +46,7 @@ WORLDS = {
 }
 
 
-SKEWED = {"d2_n8", "d12_n16_hpa"}
+SKEWED = {"d2_n8"}  # (d12_n16_hpa: more than four deployments keep the lockstep kernel)
 
 
 @pytest.mark.parametrize("name", list(WORLDS))

@@ -100,6 +100,8 @@ def world(name):
 
 NAMES = ["d2_n8", "d2_n8_overrides", "d2_n16_limits", "d3_n8_static", "d4_n16_rules", "d4_n8_delay0",
          "d4_n16_delay3", "d8_n16", "d12_n16", "config1_static12"]
+# more than four deployments keep the lockstep kernel (its state would spill: slower, sk_eligible)
+SKEWED = {n for n in NAMES if n not in ("d8_n16", "d12_n16", "config1_static12")}
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -108,7 +110,7 @@ def test_skewed_schedule_matches_oracle_and_lockstep(engine, name):
     load = po.gen_load(configs.trace_gen(23), spec.n_steps, len(spec.deploys), sc.n, first_id=sc.first_id)
     try:
         rs, ts = run_engine(engine, spec, sc, load=load, traj=True)
-        assert engine.last_engine()[0] == 5, "the world should run on the lane-skewed schedule"
+        assert engine.last_engine()[0] == (5 if name in SKEWED else 1), "engine choice"
         engine.set_engine(2)
         rl, tl = run_engine(engine, spec, sc, load=load, traj=True)
         assert engine.last_engine()[0] == 1
@@ -131,7 +133,7 @@ def test_skewed_schedule_summary_mode(engine):
 
 
 def test_skewed_schedule_not_used_where_it_does_not_hold(engine):
-    """KEDA, drift, detail and 15 s sync worlds keep the lockstep kernel."""
+    """KEDA, drift and 15 s sync worlds keep the lockstep kernel."""
     spec, sc = world("d2_n8")
     load = po.gen_load(configs.trace_gen(31), spec.n_steps, 2, sc.n, first_id=sc.first_id)
     for mut in ("keda", "drift", "sync15"):
