@@ -485,6 +485,133 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
   }
 }
 
+// The same GEMM with the operand fragments staged once per workgroup: every
+// k-step's nrt + nct distinct fragments (<= 16 KB) are loaded by the 8 waves
+// together (wave w loads fragments w and w + 8) into registers PG_PF k-steps
+// ahead, written to an LDS double buffer one k-step ahead, and each wave reads
+// its RPW + CPW fragments from LDS: global / L1 traffic is the unique 16 KB per
+// k-step instead of the waves' 48 KB (dW2), one barrier per k-step.
+#ifndef PG_PF
+#define PG_PF 8  // (A/B at 250k x 60: 2 / 4 / 8 k-steps 23.23 / 22.97 / 22.40 ms per gradient, unstaged 23.39)
+#endif
+// f(integral_constant<E>) for E = B .. N - 1 (compile-time register indices)
+template <int B, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < N) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, N>(f);
+  }
+}
+template <int RPW, int CPW>
+__global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_lds_kernel(WgradParams q) {
+  static_assert(RPW * CPW <= 8, "accumulators");
+  constexpr int PF = PG_PF;  // k-steps in flight in registers (power of two)
+  static_assert(PF >= 2 && (PF & (PF - 1)) == 0, "PG_PF");
+  __shared__ bf16x8 sf[2][16][WAVE];  // [buffer][fragment][lane]: 32 KB
+  const int lane = threadIdx.x & (WAVE - 1), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+  const int r = lane & 31, h = lane >> 5;
+  const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32, nf = nrt + nct;  // <= 16 (launch_pg_wgrad)
+  const int wc = nct / CPW, wr = nrt / RPW;
+  const bool comp = w < wr * wc;  // this wave accumulates (all 8 load)
+  const int g = comp ? w / wc : 0, rt0 = g * RPW, ct0 = comp ? (w % wc) * CPW : 0;
+  const int64_t chunk = (q.Mpad / 16 + q.splits - 1) / q.splits * 16;
+  const int64_t m0 = min((int64_t)blockIdx.x * chunk, q.Mpad), m1 = min(m0 + chunk, q.Mpad);
+  const int jb = comp && q.bpart && g < CPW ? g : -1;
+  const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  const short one = 0x3F80;
+  const bf16x8 ones = r == 0 ? bf16x8{one, one, one, one, one, one, one, one} : z;
+  auto chunk_rsrc = [&](const uint16_t* base, int U) {
+    const uint64_t a = (uint64_t)(base + (m0 >> 4) * U * 16);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(((m1 - m0) >> 4) * U * 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rsa = chunk_rsrc(q.A, q.KA), rsb = chunk_rsrc(q.B, q.KB);
+  // the two fragments this wave loads (f = w, w + 8; none past nf): operand,
+  // lane offset (a unit past KA / KB reads out of range: zero) and row-block stride
+  int lf[2];
+  bool la[2], lv[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int f = w + 8 * e;
+    lv[e] = f < nf;
+    la[e] = f < nrt;
+    const int u = (la[e] ? f : f - nrt) * 32 + r;
+    lf[e] = (u < (la[e] ? q.KA : q.KB)) ? u * 32 + 16 * h : 0x40000000;
+  }
+  const int sa = q.KA * 32, sb = q.KB * 32;
+  const int nblk = (int)((m1 - m0) >> 4);
+  bf16x8 G[PF][2];
+  auto gload = [&](int blk, auto E) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      G[E][e] = z;
+      if (lv[e] && blk < nblk)  // wave-uniform
+        G[E][e] = __builtin_bit_cast(bf16x8, la[e] ? __builtin_amdgcn_raw_buffer_load_b128(rsa, lf[e], blk * sa, 0)
+                                                    : __builtin_amdgcn_raw_buffer_load_b128(rsb, lf[e], blk * sb, 0));
+    }
+  };
+  auto lwrite = [&](int buf, auto E) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+      if (lv[e]) sf[buf][w + 8 * e][lane] = G[E][e];
+  };
+  f32x16 c[RPW][CPW], cb = zero16();
+#pragma unroll
+  for (int i = 0; i < RPW; ++i)
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) c[i][j] = zero16();
+  // prologue: k-steps 0 .. PF - 1 in flight, k-step 0 in LDS buffer 0
+  static_for<0, PF>([&](auto E) { gload(decltype(E)::value, E); });
+  lwrite(0, std::integral_constant<int, 0>{});
+  __syncthreads();
+  // k-step blk: its fragments in LDS buffer blk & 1, k-steps blk + 1 .. blk + PF - 1
+  // in registers (G[(blk + k) % PF]); k-step blk + 1 goes to the other buffer (its
+  // readers of k-step blk - 1 passed the last barrier), G[blk % PF] is refilled
+  // with k-step blk + PF. PF trips per loop keep every G index a constant.
+  auto kstep = [&](int blk, auto E) {
+    constexpr int e0 = decltype(E)::value, e1 = (e0 + 1) % PF;
+    const int bufc = blk & 1;
+    if (blk + 1 < nblk) lwrite(bufc ^ 1, std::integral_constant<int, e1>{});
+    gload(blk + PF, E);
+    if (comp) {  // wave-uniform
+      bf16x8 xa[RPW], xb[CPW];
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) xa[i] = sf[bufc][rt0 + i][lane];
+#pragma unroll
+      for (int j = 0; j < CPW; ++j) xb[j] = sf[bufc][nrt + ct0 + j][lane];
+#pragma unroll
+      for (int j = 0; j < CPW; ++j) {
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) c[i][j] = mfma(xa[i], xb[j], c[i][j]);
+        if (j == jb) cb = mfma(ones, xb[j], cb);
+      }
+    }
+    __syncthreads();
+  };
+  for (int blk = 0; blk < nblk; blk += PF) {
+    static_for<0, PF>([&](auto E) {
+      if (blk + decltype(E)::value < nblk) kstep(blk + decltype(E)::value, E);
+    });
+  }
+  if (!comp) return;
+  float* out = q.part + (int64_t)blockIdx.x * q.pstride;
+#pragma unroll
+  for (int i = 0; i < RPW; ++i)
+#pragma unroll
+    for (int j = 0; j < CPW; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int a = (rt0 + i) * 32 + (k & 3) + 8 * (k >> 2) + 4 * h, b = (ct0 + j) * 32 + r;
+        if (a < q.KA && b < q.KB) out[(int64_t)a * q.KB + b] = c[i][j][k];
+      }
+  if (jb >= 0 && h == 0) {
+    const int b = (ct0 + jb) * 32 + r;
+    if (b < q.KB) q.bpart[(int64_t)blockIdx.x * q.pstride + b] = cb[0];
+  }
+}
+
 // out = sum of the splits' partials in split order (acc: added to out, the
 // running sum over row chunks in chunk order)
 __global__ void __launch_bounds__(256) pg_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
@@ -515,6 +642,17 @@ hipError_t launch_pg_wgrad(const WgradParams& q, hipStream_t s) {
   // eight wave blocks over the output tiles
   const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32;
   const dim3 grid((unsigned)q.splits), block(64 * WG_WAVES);
+#ifndef PG_WGRAD_LDS  // A/B of the operand staging (variant builds)
+#define PG_WGRAD_LDS 1
+#endif
+  // dW2 (16 distinct fragments per k-step, each wave reading 6: 48 KB through
+  // L1 per k-step unstaged) stages them in LDS: 4.8 -> 2.5 ms per gradient at
+  // 250k x 60; dW1 / dW3 (10 / 9 distinct, 3 / 2 per wave) measured 1.9 / 1.3 ms
+  // unstaged against 1.9 / 1.6 ms staged (profiles/round6/config5_grad_kernel_stats*.csv)
+  if (PG_WGRAD_LDS && nrt == 8 && nct == 8) {
+    hipLaunchKernelGGL((pg_wgrad_lds_kernel<2, 4>), grid, block, 0, s, q);  // dW2 (+ db2)
+    return hipGetLastError();
+  }
   if (nrt == 8 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 4>), grid, block, 0, s, q);       // dW2 (+ db2)
   else if (nrt == 2 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 1>), grid, block, 0, s, q);  // dW1 (+ db1)
   else if (nrt == 8 && nct == 1) hipLaunchKernelGGL((pg_wgrad_kernel<1, 1>), grid, block, 0, s, q);  // dW3 (+ db3)
