@@ -999,7 +999,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   // per deployment, from the lane's last full step: the step keeps the replica
   // count iff usage < q_ulim and (usage >= q_pge or t <= q_hold); usage >=
   // q_slo is an SLO miss
-  int q_ulim[SKD], q_pge[SKD], q_hold[SKD], q_slo[SKD];
+  int q_ulim[SKD], q_pge[SKD], q_hold[SKD], q_slo[SKD], q_rcap[SKD];  // q_rcap: ready pods * CPU limit
   float q_R[SKD];          // max over ready slots of pods / allocatable CPU (saturation bound)
   long long q_W[SKD];      // sum over ready slots of dyn_nw_per_m * pods
   uint32_t q_usum[SKD];    // sum of the quiet steps' upp since the flush
@@ -1028,7 +1028,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   int sks_why = 0;
 #pragma unroll
   for (int d = 0; d < SKD; ++d) {
-    q_ulim[d] = 0; q_pge[d] = 0; q_hold[d] = 0; q_slo[d] = UQ;
+    q_ulim[d] = 0; q_pge[d] = 0; q_hold[d] = 0; q_slo[d] = UQ; q_rcap[d] = UQ;
     q_R[d] = 0.f; q_W[d] = 0; q_usum[d] = 0; q_rawm[d] = 0; q_band[d] = 0;
 #pragma unroll
     for (int s = 0; s < SKS; ++s) Lq[s][d] = 0;
@@ -1143,6 +1143,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       reps += cur;
       q_W[d] = Wd[d];
       q_R[d] = Rd[d];
+      q_rcap[d] = dp.limit > 0 ? (int)min((long long)rd * dp.limit, (long long)UQ) : UQ;
       int ulim = UQ, pge = 0, slo_thr = UQ, hold = UQ;
       if (dp.scaler == CCKA_SCALER_HPA) {
         const int minr = dp.minr, mx = maxr[d], tg = target[d];
@@ -1237,6 +1238,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       // minus its pods' requests), summed by capacity type; branch-free, every
       // slot's type read unconditionally so that the LDS reads issue together
       int fcs[MAXN], fms[MAXN], fps[MAXN];
+      int gwk = 0x7fffffff;
       int ac0 = 0, ac1 = 0, am0 = 0, am1 = 0, ap0 = 0, ap1 = 0;
 #pragma unroll
       for (int n = 0; n < MAXN; ++n) {
@@ -1273,8 +1275,13 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
         vm -= own ? fms[n] : 0;
         vp -= own ? fps[n] : 0;
         const bool pass = pods == 0 || (pol == CCKA_WHEN_EMPTY_OR_UNDERUTILIZED && c <= vc && m <= vm && pods <= vp);
-        if (((used & rdy) >> n & 1u) && thr > t && pass) nx = min(nx, thr);
+        if (((used & rdy) >> n & 1u) && thr > t && pass) gwk = min(gwk, thr);
       }
+      // the disruption phase's own wake (exact for the same reason): the next
+      // full step evaluates it only when the gate may admit a candidate or
+      // something it depends on moved (g_dirty)
+      g_wake = gwk;
+      nx = min(nx, gwk);
     }
     if (unplaced) nx = t + 1;
     if constexpr (kSKS) {
@@ -2970,8 +2977,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
             us[d] = 0;
             ge[d] = false;
             if (d >= D) continue;
-            // usage clamped by the pods' CPU limit (ready pods * limit, 64-bit)
-            us[d] = dep[d].limit > 0 ? (int)min((long long)Lq[0][d], (long long)rpods[d] * dep[d].limit) : Lq[0][d];
+            us[d] = min(Lq[0][d], q_rcap[d]);  // usage clamped by the pods' CPU limit
             if (dep[d].scaler != CCKA_SCALER_HPA) continue;
             ge[d] = us[d] >= q_pge[d];
             ok = ok && (uint32_t)us[d] < (uint32_t)q_ulim[d] && (ge[d] || tc <= q_hold[d]);
