@@ -109,6 +109,11 @@ struct ccka_ctx {
   double* d_wc0 = nullptr;    // one zero carbon weight (the offer table's score is the price)
   int JT = 0, NW = 0;
   int engine_mode = 0;       // 0 auto, 1 general kernel only, 2 general kernel in lockstep (ccka_debug_engine)
+  bool sk_coop_f2 = false;   // skewed schedule: keep the wave-cooperative provisioning (ccka_debug_engine 3)
+#ifndef SK_LANE_F2
+#define SK_LANE_F2 0
+#endif
+  bool sk_lane_f2 = SK_LANE_F2 != 0;  // lane-local provisioning compiled in (variant builds)
   unsigned long long* d_stamps = nullptr;
   int lpw = 0;               // scenarios per wave of the single-deployment kernel (0 = automatic)
   int occ = 0;               // its register-allocation occupancy target (0 = automatic)
@@ -1100,6 +1105,7 @@ static int setup_general(ccka_ctx* c, int32_t trajectory, int* block_out, size_t
       k.hist = c->d_hist;
     }
   }
+  k.lds_lclaims = -1;
   k.t0 = 0;
   k.t1 = w.n_steps;
   k.state = nullptr;
@@ -1234,6 +1240,15 @@ int ccka_rollout_async(ccka_ctx* c, int32_t trajectory) {
     if (sk) {
       if ((rc = sk_trace(c)) != CCKA_OK) return rc;
       if (c->load_nt_dp) k.load_nt = c->d_load_nt;
+      // lane-local provisioning for small catalogs: one LDS column of NodeClaims
+      // per lane ([claim][field][lane] ints) when it fits beside the rest
+      int dmax, nmax;
+      kernel_dims(w.n_deploy, w.max_nodes, &dmax, &nmax);
+      const size_t col = ((lds + 15) & ~(size_t)15), need = (size_t)nmax * (7 + dmax) * block * 4;
+      if (!c->sk_coop_f2 && c->sk_lane_f2 && w.n_types <= 64 && col + need <= 160 * 1024) {
+        k.lds_lclaims = (int32_t)col;
+        lds = col + need;
+      }
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_mid, c->stream));
@@ -2441,10 +2456,13 @@ int ccka_debug_ablate(ccka_ctx* c, int32_t mask) {
 
 // Internal (not in include/ccka.h): 0 = choose the engine automatically,
 // 1 = always the general kernel (tests compare both engines), 2 = the general
-// kernel in lockstep (no lane-skewed schedule for several deployments).
+// kernel in lockstep (no lane-skewed schedule for several deployments), 3 =
+// automatic with the skewed schedule's provisioning on the wave-cooperative scans.
 int ccka_debug_engine(ccka_ctx* c, int32_t mode) {
-  if (!c || mode < 0 || mode > 2) return CCKA_EINVAL;
-  c->engine_mode = mode;
+  if (!c || mode < 0 || mode > 3) return CCKA_EINVAL;
+  // 3: automatic, with the skewed schedule's wave-cooperative provisioning (A/B of the lane-local one)
+  c->sk_coop_f2 = mode == 3;
+  c->engine_mode = mode == 3 ? 0 : mode;
   return CCKA_OK;
 }
 

@@ -86,6 +86,8 @@ struct KParams {
   int64_t first_id;
   int32_t T, D, K, Z, R, P, maxn, span, all_hours;
   int32_t lds_off_cap1, lds_off_tile, lds_off_claims, lds_off_misc, lds_off_ci;
+  int32_t lds_lclaims;  // SK: per-lane NodeClaim columns for the lane-local F2 (-1: the cooperative scans)
+  int32_t _kpad;
   int32_t ablate;  // profiling-only phase switches (0 in every real run)
   unsigned long long* stamps;  // diagnostic phase cycle totals (GK_STAMPS builds only; nullptr otherwise)
   int32_t prov[CCKA_MAX_DEPLOY];
@@ -154,6 +156,7 @@ hipError_t launch_rollout_policy(const KParams& p, size_t lds, int pol, hipStrea
 hipError_t launch_rollout_multi(const KParams& p, int block, size_t lds, hipStream_t s);
 // two to four deployments on the lane-skewed schedule (rollout_sk.hip)
 hipError_t launch_rollout_sk(const KParams& p, int block, size_t lds, hipStream_t s);
+hipError_t launch_rollout_sk416(const KParams& p, int block, size_t lds, hipStream_t s);  // <4, 16> (rollout_sk416.hip)
 // [T][D][NL] -> [NL][T][DP] (DP >= D, a power of two <= 16; padded with 0) for the skewed schedule
 hipError_t launch_trace_nt(const int32_t* in, int32_t* out, int64_t NL, int64_t T, int32_t D, int32_t DP,
                            hipStream_t s);

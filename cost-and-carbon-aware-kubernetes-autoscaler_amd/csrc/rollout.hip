@@ -988,6 +988,9 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   constexpr int SKS = SK ? (SK_S_V) : 1;  // quiet steps per iteration and lane
   constexpr int SKD = SK ? DMAX : 1;
   constexpr int UQ = 0x7fffffff;  // "any usage" threshold
+#ifndef SK_LANE_F2  // lane-local provisioning on the skewed schedule (variant builds)
+#define SK_LANE_F2 0
+#endif
 #ifndef SK_K_V  // full-step cadence in passes (variant builds)
 #define SK_K_V 1
 #endif
@@ -1024,7 +1027,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
 #else
   constexpr bool kSKS = false;
 #endif
-  uint32_t sks_c[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t sks_c[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // 11: lanes served by provisioning
   int sks_why = 0;
 #pragma unroll
   for (int d = 0; d < SKD; ++d) {
@@ -1775,6 +1778,181 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
           }
         }
       }
+    } else if (SK && SK_LANE_F2 && p.lds_lclaims >= 0) {
+      // lane-local F2 (variant builds, SK_LANE_F2; measured 1-4 % slower than the
+      // cooperative scans on 2 / 4 deployments x 8 / 16 slots): every
+      // lane that needs NodeClaims builds and launches them itself, by the
+      // cooperative path's rules in the same order (claims of this step in
+      // creation order, the first admitting pool with j > 0, the launch argmin
+      // over (score, type, zone, capacity type) in index order), so the lanes
+      // of a run provision in parallel instead of one after another; each
+      // lane's claims in its own LDS column [claim][field][lane]
+      int anyp = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) anyp |= pend[d] > 0;
+      const uint32_t free_mask = ~used & slot_mask;
+      if (active && anyp && free_mask != 0) {
+        if constexpr (kSKS) sks_c[11]++;
+        uint32_t lfree = free_mask;
+        int use0[CCKA_MAX_POOLS], usenow[CCKA_MAX_POOLS];
+#pragma unroll
+        for (int q = 0; q < CCKA_MAX_POOLS; ++q) { use0[q] = puse[q]; usenow[q] = puse[q]; }
+        auto mem_now = [&](int q) { return w->pools[q].limit_mem_mi >= 0 ? pool_mem(q) : 0; };
+        constexpr int CW = CLAIM_FIXED + DMAX;
+        int* const CLb = reinterpret_cast<int*>(smem + p.lds_lclaims);
+        const int nthr = (int)blockDim.x;
+        auto CLA = [&](int c, int f) -> int& { return CLb[(c * CW + f) * nthr + tid]; };
+        // j: most pods of the deployment any candidate type holds on top of the sums
+        auto claim_j = [&](uint32_t zm, uint32_t cm, int s_cpu, int s_mem, int s_pods, int rc, int rm, int use, int limit,
+                           int usem, int limitm) {
+          int best = 0;
+          for (int k = 0; k < L.K; ++k) {
+            if (!limit_ok(L, k, use, limit, usem, limitm)) continue;
+            const int f = type_fit<DMAX>(L, k, s_cpu, s_mem, s_pods, rc, rm);
+            if (f <= best) continue;
+            if (!type_offered(L, rlx, k, zm, cm)) continue;
+            best = f;
+          }
+          return best;
+        };
+        int ncl = 0;
+        for (int oi = 0; oi < D; ++oi) {
+          const int d = p.prov[oi];
+          int rem = 0, rc = 0, rm = 0;
+          uint32_t csel = 0;
+#pragma unroll
+          for (int e = 0; e < DMAX; ++e)
+            if (e == d) { rem = pend[e]; csel = capsel[e]; rc = dep[e].req_cpu; rm = dep[e].req_mem; }
+          if (rem <= 0) continue;
+          for (int c = 0; c < ncl && rem > 0; ++c) {
+            const int cpool = CLA(c, 0);
+            const uint32_t cm = (uint32_t)CLA(c, 1) & csel;
+            if (!cm) continue;
+            int climit = 0;
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) climit = plimit[q];
+            int u0 = 0;
+#pragma unroll
+            for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) u0 = use0[q];
+            const int j = claim_j((uint32_t)CLA(c, 2), cm, CLA(c, 4), CLA(c, 5), CLA(c, 6), rc, rm, u0, climit,
+                                  mem_now(cpool), w->pools[cpool].limit_mem_mi);
+            if (j <= 0) continue;
+            const int k = min(j, rem);
+            CLA(c, 1) = (int)cm;
+            CLA(c, 4) += k * rc;
+            CLA(c, 5) += k * rm;
+            CLA(c, 6) += k;
+            CLA(c, CLAIM_FIXED + d) += k;
+            rem -= k;
+          }
+          while (rem > 0 && lfree) {
+            const int slot = __ffs((int)lfree) - 1;
+            int chosen = -1, jj = 0;
+            uint32_t czm = 0, ccm = 0;
+            for (int q = 0; q < NP && chosen < 0; ++q) {
+              uint32_t zq = 0, cq = 0;
+              int u0 = 0, lq = 0;
+#pragma unroll
+              for (int qq = 0; qq < CCKA_MAX_POOLS; ++qq)
+                if (qq == q) { zq = pzm[qq]; cq = pcm[qq]; u0 = use0[qq]; lq = plimit[qq]; }
+              const uint32_t cm = cq & csel;
+              if (!cm) continue;
+              const int j = claim_j(zq, cm, 0, 0, 0, rc, rm, u0, lq, mem_now(q), w->pools[q].limit_mem_mi);
+              if (j > 0) { chosen = q; jj = j; czm = zq; ccm = cm; }
+            }
+            if (chosen < 0) break;
+            const int k = min(jj, rem);
+            CLA(ncl, 0) = chosen;
+            CLA(ncl, 1) = (int)ccm;
+            CLA(ncl, 2) = (int)czm;
+            CLA(ncl, 3) = slot;
+            CLA(ncl, 4) = k * rc;
+            CLA(ncl, 5) = k * rm;
+            CLA(ncl, 6) = k;
+#pragma unroll
+            for (int e = 0; e < DMAX; ++e) CLA(ncl, CLAIM_FIXED + e) = e == d ? k : 0;
+            ncl++;
+            lfree &= ~(1u << slot);
+            rem -= k;
+          }
+        }
+        // launch in creation order (wave_launch's rule, lane-local)
+        for (int c = 0; c < ncl; ++c) {
+          const int cpool = CLA(c, 0);
+          const uint32_t zm = (uint32_t)CLA(c, 2), cm = (uint32_t)CLA(c, 1);
+          const int s_cpu = CLA(c, 4), s_mem = CLA(c, 5), s_pods = CLA(c, 6);
+          int climit = 0, unow = 0;
+#pragma unroll
+          for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) { climit = plimit[q]; unow = usenow[q]; }
+          const int usem = mem_now(cpool), limitm = w->pools[cpool].limit_mem_mi;
+          bool spot_only = false;
+          if (cm & CCKA_CAP_SPOT) {
+            for (int k = 0; k < L.K && !spot_only; ++k) {
+              if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, unow, climit, usem, limitm)) continue;
+              for (int z = 0; z < L.Z; ++z)
+                if ((zm >> z & 1u) && tprice(L, rlx, k, z, 0) > 0) { spot_only = true; break; }
+            }
+          }
+          double bs = __builtin_inf();
+          int bi = 0x7fffffff;
+          for (int k = 0; k < L.K; ++k) {
+            if (!type_holds<DMAX>(L, k, s_cpu, s_mem, s_pods) || !limit_ok(L, k, unow, climit, usem, limitm)) continue;
+            const double carbon = L.types[k].p_ref_w * ci_gpwh;
+            for (int z = 0; z < L.Z; ++z) {
+              if (!(zm >> z & 1u)) continue;
+              for (int cc = 0; cc < 2; ++cc) {
+                if (!(cm & (uint32_t)capbit(cc))) continue;
+                if (spot_only && cc != 0) continue;
+                const int pr = tprice(L, rlx, k, z, cc);
+                if (pr <= 0) continue;
+                const double score = (double)pr + wc1000 * carbon;
+                if (score < bs) { bs = score; bi = (k * L.Z + z) * 2 + cc; }
+              }
+            }
+          }
+          if (bi == 0x7fffffff) continue;
+          const int bc = bi & 1, bz = (bi >> 1) % Z, bk = (bi >> 1) / Z;
+          const int vcpu_m = L.types[bk].vcpu * 1000;
+#pragma unroll
+          for (int q = 0; q < CCKA_MAX_POOLS; ++q) if (q == cpool) usenow[q] += vcpu_m;
+          const int slot = CLA(c, 3);
+          const uint32_t choice = (uint32_t)bk | (uint32_t)bz << 12 | (uint32_t)bc << 14 | (uint32_t)cpool << 16;
+          const bool now_ready = delay == 0;
+          const int price = tprice(L, rlx, bk, bz, bc);
+          const int cap = DMAX == 1 ? L.cap1[bk] : 0;
+#pragma unroll
+          for (int n = 0; n < MAXN; ++n) {
+            if (n == slot) {
+              ninfo[n] = ni_make(cpool, bk, bz, bc);
+              nready[n] = t + delay;
+              nlast[n] = t;
+              nprice[n] = price;
+              ncap[n] = cap;
+#pragma unroll
+              for (int e = 0; e < DMAX; ++e) {
+                const int k = e < D ? CLA(c, CLAIM_FIXED + e) : 0;
+                npods[n][e] = k;
+                placed[e] += k;
+                if (now_ready) rpods[e] += k;
+              }
+            }
+          }
+          used |= 1u << slot;
+          if (now_ready) rdy |= 1u << slot;
+          else next_ready = min(next_ready, t + delay);
+#pragma unroll
+          for (int q = 0; q < CCKA_MAX_POOLS; ++q)
+            if (q == cpool) puse[q] += vcpu_m;
+          if (bc == 0) nsp++; else nod++;
+          burn += price;
+          launches++;
+          last_choice = choice;
+          hash = (hash ^ choice) * 16777619u;
+          step_last_type = bk;
+          flags |= 2u;
+          if (now_ready) g_dirty = true;
+        }
+      }
     } else {
       int anyp = 0;
 #pragma unroll
@@ -1783,6 +1961,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
       unsigned long long need = __ballot(active && anyp && free_mask != 0 && !ablated(p.ablate, 2));
       while (need) {
         const int ld = __ffsll((long long)need) - 1;
+        if constexpr (kSKS) sks_c[11] += lane == ld ? 1 : 0;
         need &= need - 1;
         // broadcast the leader's state
         const int lrl = rdl(rlx, ld);
@@ -3061,7 +3240,7 @@ __global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 
   if constexpr (kSKS) {
     if (p.stamps) {
 #pragma unroll
-      for (int k = 0; k < 11; ++k) atomicAdd(&p.stamps[k], (unsigned long long)sks_c[k]);
+      for (int k = 0; k < 12; ++k) atomicAdd(&p.stamps[k], (unsigned long long)sks_c[k]);
     }
   }
   if (!active) return;

@@ -62,8 +62,8 @@ hipError_t launch_rollout_sk(const KParams& p, int block, size_t lds, hipStream_
     hipLaunchKernelGGL((rollout_kernel<2, 16, 0, 1>), dim3(grid), dim3(block), lds, s, p);
   else if (dmax == 4 && nmax == 8)
     hipLaunchKernelGGL((rollout_kernel<4, 8, 0, 1>), dim3(grid), dim3(block), lds, s, p);
-  else if (dmax == 4)
-    hipLaunchKernelGGL((rollout_kernel<4, 16, 0, 1>), dim3(grid), dim3(block), lds, s, p);
+  else if (dmax == 4)  // rollout_sk416.hip
+    return launch_rollout_sk416(p, block, lds, s);
   else
     return hipErrorInvalidValue;
 #endif

@@ -149,3 +149,21 @@ def test_skewed_schedule_not_used_where_it_does_not_hold(engine):
         rc, tc = oracle(s2, sc, load, traj=True, threads=THREADS)
         compare(rg, rc, tg, tc)
     del spec
+
+
+@pytest.mark.parametrize("name", ["d2_n8_overrides", "d2_n16_limits", "d4_n8_delay0"])
+def test_skewed_schedule_cooperative_provisioning(engine, name):
+    """ccka_debug_engine(3) (the skewed schedule with the wave-cooperative scans
+    forced; builds with SK_LANE_F2 otherwise provision lane-locally for small
+    catalogs) and the default give the oracle's launches, bit for bit."""
+    spec, sc = world(name)
+    load = po.gen_load(configs.trace_gen(37), spec.n_steps, len(spec.deploys), sc.n, first_id=sc.first_id)
+    rc, tc = oracle(spec, sc, load, traj=True, threads=THREADS)
+    for mode in (0, 3):
+        try:
+            engine.set_engine(mode)
+            rg, tg = run_engine(engine, spec, sc, load=load, traj=True)
+            assert engine.last_engine()[0] == 5
+        finally:
+            engine.set_engine(0)
+        compare(rg, rc, tg, tc)

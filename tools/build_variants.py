@@ -40,7 +40,7 @@ for arg in sys.argv[1:]:
 for name, out, obj, p in procs:
     assert p.wait() == 0, name
     others = [os.path.join(CSRC, "build", f) for f in ("rollout.o", "rollout_multi.o", "rollout_pol.o", "rollout_sk.o",
-                                                       "rollout_d1.o", "rollout_pool.o", "sweep.o", "mlp.o", "pg.o",
+                                                       "rollout_sk416.o", "rollout_d1.o", "rollout_pool.o", "sweep.o", "mlp.o", "pg.o",
                                                        "ccka_abi.o") if f != os.path.basename(obj)]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     os.path.join(out, "libccka.so"), obj, *others, "-L/opt/rocm/lib", "-lrccl",

@@ -20,7 +20,12 @@ if not TRAJ:
 STAMPS = "--stamps" in sys.argv
 if STAMPS:
     sys.argv.remove("--stamps")
-VAR = None  # --lib NAME: another variant under csrc/build/variants (timing only)
+MODE = None  # --mode M: ccka_debug_engine(M) (3: the cooperative provisioning scans)
+if "--mode" in sys.argv:
+    k = sys.argv.index("--mode")
+    MODE = int(sys.argv[k + 1])
+    del sys.argv[k:k + 2]
+VAR = None  # --lib NAME: another variant under csrc/build/variants (timing only); "main": the main build
 if "--lib" in sys.argv:
     k = sys.argv.index("--lib")
     VAR = sys.argv[k + 1]
@@ -29,6 +34,8 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 1440
 lib = os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build", "variants", VAR or ("skgks" if STAMPS else "skstats"),
                    "libccka.so")
+if VAR == "main":
+    lib = os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build", "libccka.so")
 e = Engine(0, lib_path=lib)
 e.lib.ccka_debug_ablate.argtypes = [C.c_void_p, C.c_int32]
 e.lib.ccka_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
@@ -36,6 +43,8 @@ spec = configs.config2_world(n_steps=T)
 spec.deploys = [configs.deployment(abi.SCALER_HPA, replicas0=3, max_r=30, req_cpu=(200, 300)[d],
                                    target=(70, 60)[d]) for d in range(2)]
 sc = configs.hpa_scenarios(N)
+if MODE is not None:
+    e.set_engine(MODE)
 e.set_world(spec)
 e.set_scenarios(sc)
 e.gen_load(configs.trace_gen())
@@ -64,7 +73,8 @@ if STAMPS:
     sys.exit(0)
 names = ["stall: disruption pending (g_dirty)", "stall: pods not placed", "stall: consolidation wake",
          "stall: node ready", "stall: hour / peak boundary", "stall: HPA outside thresholds",
-         "live lane-passes", "lane full steps", "lane quiet steps", "wave full-step runs", "wave passes"]
+         "live lane-passes", "lane full steps", "lane quiet steps", "wave full-step runs", "wave passes",
+         "lanes served by provisioning"]
 waves = (N + 63) // 64
 for k, nm in enumerate(names):
     print(f"{nm:40s} {st[k]:14d}  per scenario {st[k] / N:10.2f}  per wave {st[k] / waves:10.2f}")
