@@ -622,8 +622,12 @@ constexpr bool kGKS = false;
 // step over the register rings, every hour's price tiles in LDS, no detail,
 // drift, replacement or multi-node consolidation, the whole horizon in one
 // launch. Trajectory records scenario-major [N][T].
+#ifndef SK_OCC2  // skewed instantiations at two waves per SIMD (variant builds)
+#define SK_OCC2 0
+#endif
 template <int DMAX, int MAXN, int POL = 0, int SK = 0>
-__global__ void __launch_bounds__(256, (POL == 0 && DMAX == 1 && MAXN <= 8) ? 2 : 1) rollout_kernel(KParams p) {
+__global__ void __launch_bounds__(256, ((POL == 0 && DMAX == 1 && MAXN <= 8) || (SK && SK_OCC2)) ? 2 : 1)
+    rollout_kernel(KParams p) {
   static_assert(POL == 0 || (DMAX == 1 && MAXN <= 8), "fused closed loop: one deployment, <= 8 slots");
   static_assert(SK == 0 || POL == 0, "the skewed schedule is the rule-based rollout's");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
