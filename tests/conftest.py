@@ -18,6 +18,7 @@ def pytest_configure(config):
 def engine():
     from ccka.engine import Engine
 
-    e = Engine(0)
+    # CCKA_TEST_LIB: run the suite against a variant build (A/B parity of a build switch)
+    e = Engine(0, lib_path=os.environ.get("CCKA_TEST_LIB") or None)
     yield e
     e.close()

@@ -30,9 +30,14 @@ if "--lib" in sys.argv:
     k = sys.argv.index("--lib")
     VAR = sys.argv[k + 1]
     del sys.argv[k:k + 2]
+SLIB = None  # --slib NAME: the counter / stamp variant to read (default skstats / skgks)
+if "--slib" in sys.argv:
+    k = sys.argv.index("--slib")
+    SLIB = sys.argv[k + 1]
+    del sys.argv[k:k + 2]
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 1440
-lib = os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build", "variants", VAR or ("skgks" if STAMPS else "skstats"),
+lib = os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build", "variants", VAR or SLIB or ("skgks" if STAMPS else "skstats"),
                    "libccka.so")
 if VAR == "main":
     lib = os.path.join(ROOT, "cost-and-carbon-aware-kubernetes-autoscaler_amd", "csrc", "build", "libccka.so")
