@@ -392,7 +392,14 @@ __global__ void __launch_bounds__(256, 1) pg_rows_kernel(PgRowsParams p) {
 // split order (deterministic), all three GEMMs in one launch.
 // ---------------------------------------------------------------------------
 constexpr int WG_WAVES = 8;
-template <int RPW, int CPW>
+template <int B, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < N) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, N>(f);
+  }
+}
+template <int RPW, int CPW, int PD = 2>
 __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams q) {
   static_assert(RPW * CPW <= 8, "accumulators");
   // w wave-uniform in an SGPR (the loads' resources and offsets derive from it)
@@ -438,7 +445,7 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
   for (int i = 0; i < RPW; ++i)
 #pragma unroll
     for (int j = 0; j < CPW; ++j) c[i][j] = zero16();
-  bf16x8 xa[2][RPW], xb[2][CPW];
+  bf16x8 xa[PD][RPW], xb[PD][CPW];  // PD k-steps of fragments: this one's and PD - 1 in flight
   auto load = [&](int blk, auto S) {  // row block blk of the chunk into buffer S
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
@@ -448,11 +455,12 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
       xb[S][j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsb, ob[j], blk * sb, 0));
   };
   const int nblk = (int)((m1 - m0) >> 4);
-  if (nblk > 0) load(0, std::integral_constant<int, 0>{});
-  if (nblk > 1) load(1, std::integral_constant<int, 1>{});
-  // this k-step's fragments in buffer S, the next one's in flight in 1 - S;
-  // buffer S is refilled (two k-steps ahead) once its MFMAs have read it. Two
-  // k-steps per trip keep the buffer index a compile-time constant (a
+  static_for<0, PD>([&](auto S) {
+    if (nblk > decltype(S)::value) load(decltype(S)::value, S);
+  });
+  // this k-step's fragments in buffer S, the next PD - 1 in flight in the
+  // others; buffer S is refilled (PD k-steps ahead) once its MFMAs have read
+  // it. PD k-steps per trip keep the buffer index a compile-time constant (a
   // runtime-indexed register array would live in scratch memory)
   auto kstep = [&](int blk, auto S) {
 #pragma unroll
@@ -462,11 +470,12 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
       if (j == jb) cb = mfma(ones, xb[S][j], cb);  // wave-uniform branch
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (blk + 2 < nblk) load(blk + 2, S);
+    if (blk + PD < nblk) load(blk + PD, S);
   };
-  for (int blk = 0; blk < nblk; blk += 2) {
-    kstep(blk, std::integral_constant<int, 0>{});
-    if (blk + 1 < nblk) kstep(blk + 1, std::integral_constant<int, 1>{});
+  for (int blk = 0; blk < nblk; blk += PD) {
+    static_for<0, PD>([&](auto S) {
+      if (blk + decltype(S)::value < nblk) kstep(blk + decltype(S)::value, S);
+    });
   }
   // accumulator register k: row a0 + (k&3) + 8(k>>2) + 4h, column b0 + r
   float* out = q.part + (int64_t)blockIdx.x * q.pstride;
@@ -495,13 +504,6 @@ __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_kernel(WgradParams 
 #define PG_PF 8  // (A/B at 250k x 60: 2 / 4 / 8 k-steps 23.23 / 22.97 / 22.40 ms per gradient, unstaged 23.39)
 #endif
 // f(integral_constant<E>) for E = B .. N - 1 (compile-time register indices)
-template <int B, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < N) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, N>(f);
-  }
-}
 template <int RPW, int CPW>
 __global__ void __launch_bounds__(64 * WG_WAVES, 1) pg_wgrad_lds_kernel(WgradParams q) {
   static_assert(RPW * CPW <= 8, "accumulators");
@@ -642,6 +644,16 @@ hipError_t launch_pg_wgrad(const WgradParams& q, hipStream_t s) {
   // eight wave blocks over the output tiles
   const int nrt = (q.KA + 31) / 32, nct = (q.KB + 31) / 32;
   const dim3 grid((unsigned)q.splits), block(64 * WG_WAVES);
+// k-steps of operand fragments per wave in flight + 1 (variant builds),
+// measured per launch at 250k x 60 (two launches per gradient): dW3 (one row
+// and one column tile per wave) PD 2 / 4 / 8: 0.742 / 0.653 / 0.668 ms; dW1
+// (two row tiles per wave) PD 2 / 3 / 4: 0.899 / 0.936 / 1.007 ms
+#ifndef PG_PD1  // dW1
+#define PG_PD1 2
+#endif
+#ifndef PG_PD3  // dW3
+#define PG_PD3 4
+#endif
 #ifndef PG_WGRAD_LDS  // A/B of the operand staging (variant builds)
 #define PG_WGRAD_LDS 1
 #endif
@@ -654,8 +666,8 @@ hipError_t launch_pg_wgrad(const WgradParams& q, hipStream_t s) {
     return hipGetLastError();
   }
   if (nrt == 8 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 4>), grid, block, 0, s, q);       // dW2 (+ db2)
-  else if (nrt == 2 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 1>), grid, block, 0, s, q);  // dW1 (+ db1)
-  else if (nrt == 8 && nct == 1) hipLaunchKernelGGL((pg_wgrad_kernel<1, 1>), grid, block, 0, s, q);  // dW3 (+ db3)
+  else if (nrt == 2 && nct == 8) hipLaunchKernelGGL((pg_wgrad_kernel<2, 1, PG_PD1>), grid, block, 0, s, q);  // dW1 (+ db1)
+  else if (nrt == 8 && nct == 1) hipLaunchKernelGGL((pg_wgrad_kernel<1, 1, PG_PD3>), grid, block, 0, s, q);  // dW3 (+ db3)
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
