@@ -620,8 +620,19 @@ __global__ void __launch_bounds__(256) pg_reduce_kernel(const float* __restrict_
                                                         int64_t n, int splits, int acc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // split order as one chain of additions; the loads of 16 splits issue
+  // together ahead of their adds (one dependent load per add measured 103 us
+  // per launch for 256 x 86k floats)
   float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += part[(int64_t)k * n + i];
+  int k = 0;
+  for (; k + 16 <= splits; k += 16) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = part[(int64_t)(k + j) * n + i];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
+  }
+  for (; k < splits; ++k) s += part[(int64_t)k * n + i];
   out[i] = acc ? out[i] + s : s;
 }
 
