@@ -1651,7 +1651,7 @@ static constexpr int64_t kGradFloats = 64 * 256 + 256 + 256 * 256 + 256 + 256 * 
 // only on M, never on the memory available (deterministic); M <= one chunk is
 // the unchunked computation.
 constexpr int64_t kPgChunkRows = 1LL << 23;
-constexpr int64_t kPgSplits = 256;  // weight-gradient row splits per chunk (at most)
+constexpr int64_t kPgSplits = 256;  // weight-gradient row splits per chunk (at most; 512 measured 21.8 -> 22.6 ms)
 static int64_t pg_chunk_rows(const ccka_ctx* c) { return c->pg_chunk > 0 ? c->pg_chunk : kPgChunkRows; }
 
 static int pg_backward(ccka_ctx* c, const uint16_t* x, const uint8_t* act, const float* coef, int64_t n_scen,
