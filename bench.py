@@ -442,7 +442,7 @@ def main():
 def general_dims(d, maxn):
     """The general kernel's register layout for d deployments and maxn node
     slots (kernel_dims in csrc/kparams.h)."""
-    dmax = 1 if d == 1 else 2 if d <= 2 else 4 if d <= 4 else 8 if d <= 8 else 16
+    dmax = 1 if d == 1 else 2 if d <= 2 else 4 if d <= 4 else 8 if d <= 8 else 12 if d <= 12 else 16
     return dmax, 8 if maxn <= 8 and dmax <= 4 else 16
 
 

@@ -144,7 +144,9 @@ constexpr int kPartBytes = 11 * 8;
 
 // kernel instantiation chosen for (D, max_nodes): DMAX x MAXN
 inline void kernel_dims(int D, int maxn, int* dmax, int* nmax) {
-  *dmax = D == 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : 16;
+  // (12: the reference's own 12 burst Deployments, demo_30_burst_configure.sh, without
+  // four empty deployment columns of per-lane state)
+  *dmax = D == 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : D <= 12 ? 12 : 16;
   *nmax = maxn <= 8 && *dmax <= 4 ? 8 : 16;
 }
 

@@ -1,5 +1,5 @@
 // rollout_multi.hip — the general kernel's lockstep instantiations for four or
-// more deployments (rollout_kernel<4|8|16, 8|16>). The kernel template is
+// more deployments (rollout_kernel<4|8|12|16, 8|16>). The kernel template is
 // rollout.hip's; this unit only instantiates it, so the instantiations compile
 // in parallel with rollout.hip's.
 #define CCKA_ROLLOUT_PART 1
@@ -17,6 +17,8 @@ hipError_t launch_rollout_multi(const KParams& p, int block, size_t lds, hipStre
     hipLaunchKernelGGL((rollout_kernel<4, 16>), dim3(grid), dim3(block), lds, s, p);
   else if (dmax == 8)
     hipLaunchKernelGGL((rollout_kernel<8, 16>), dim3(grid), dim3(block), lds, s, p);
+  else if (dmax == 12)
+    hipLaunchKernelGGL((rollout_kernel<12, 16>), dim3(grid), dim3(block), lds, s, p);
   else if (dmax == 16)
     hipLaunchKernelGGL((rollout_kernel<16, 16>), dim3(grid), dim3(block), lds, s, p);
   else
